@@ -1,0 +1,250 @@
+#!/usr/bin/env python
+"""Benchmark of the codec hot path: BASELINE.json's metric, Megapixels/s encode+decode.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--size 256]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+A step = nic_encode + nic_decode of one batch of `--batch` synthetic u8 256x256x3 images
+already resident in HBM (BASELINE config 2 at N=1; config 3's 8 x 64 sharding at N=8:
+weak scaling, each rank owns its own 64 images, no data-path collective).  Weights are
+the seeded 'spread' init (no trained checkpoint exists), generated on rank 0 and
+broadcast over RCCL once at setup.
+
+Rank 0 prints ONE JSON line with the driver's keys plus:
+  roofline     -- dominant kernel: algorithmic FLOP per launch / its mean launch time,
+                  measured with hipEvents on the launch stream over a timed pass;
+  layers       -- the same per layer;
+  cpu_baseline -- the NumPy oracle (fp32 BLAS, the CPU restatement of tf2_0; TF itself
+                  is not installable) on a bounded sample, rank 0 at N=1 only;
+  parity       -- PSNR of one benchmarked image's reconstruction vs the oracle.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Megapixels/sec encode+decode"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+def layer_geometry(h: int, w: int):
+    """Per-plane (FLOP, name) of every layer for an h x w input (2 x MAC)."""
+    def same(n):
+        return -(-n // 2)
+    h1, w1 = same(h), same(w)
+    h2, w2 = same(h1), same(w1)
+    h8, w8 = same(h2), same(w2)
+    g = {
+        "conv1": 2 * h1 * w1 * 1 * 32 * 25,
+        "conv2": 2 * h2 * w2 * 32 * 64 * 25,
+        "conv3": 2 * h2 * w2 * 64 * 64 * 9,
+        "conv4": 2 * h2 * w2 * 64 * 64 * 9,
+        "conv8": 2 * h8 * w8 * 64 * 32 * 25,
+        "dconv1": 2 * h8 * w8 * 32 * 64 * 25,
+        "dconv5": 2 * (2 * h8) * (2 * w8) * 64 * 64 * 9,
+        "dconv6": 2 * (2 * h8) * (2 * w8) * 64 * 64 * 9,
+        "dconv7": 2 * (2 * h8) * (2 * w8) * 64 * 64 * 25,
+        "dconv8": 2 * (4 * h8) * (4 * w8) * 64 * 1 * 25,
+    }
+    return g
+
+
+def broadcast_weights(w, dist, rank, device):
+    """RCCL broadcast of the fp32 weights from rank 0 (one flat buffer)."""
+    import torch
+
+    from neural_network_image_compression_amd import weights as W
+
+    keys = W.keys()
+    sizes = [int(np.prod(W.expected_shape(k))) for k in keys]
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=device)
+    if rank == 0:
+        flat.copy_(torch.from_numpy(np.concatenate([w[k].ravel() for k in keys])))
+    dist.broadcast(flat, src=0)
+    host = flat.cpu().numpy()
+    out, o = {}, 0
+    for k, s in zip(keys, sizes):
+        out[k] = host[o:o + s].reshape(W.expected_shape(k)).copy()
+        o += s
+    return out
+
+
+def cpu_baseline(weights, size: int, seconds: float):
+    """NumPy oracle (fp32 BLAS accumulation) on synthetic images of the same workload until
+    `seconds` of CPU work have run (at least one image)."""
+    from oracle import nic_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    rng = np.random.default_rng(1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        x = rng.integers(0, 256, (1, size, size, 3), dtype=np.uint8)
+        O.decode(weights, O.encode(weights, x, acc=np.float32), acc=np.float32)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * size * size / 1e6 / el, "unit": "MP/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} synthetic {size}x{size}x3 images, encode+decode, oracle/nic_oracle.py fp32 "
+                      f"(CPU restatement of tf2_0; TF not installable), {el:.1f} s"}
+
+
+def parity_sample(codec, x0, weights):
+    """PSNR of the GPU reconstruction of one benchmarked image vs the oracle's (fp64 acc)."""
+    import torch
+
+    from oracle import nic_oracle as O
+
+    xh = x0.cpu().numpy()
+    z = codec.encode(x0)
+    r = codec.decode(z).cpu().numpy()
+    torch.cuda.synchronize()
+    r_ref = O.decode(weights, O.encode(weights, xh))
+    return {"psnr_gpu_vs_oracle_db": round(O.psnr(r, r_ref), 2),
+            "psnr_x_gpu_db": round(O.psnr(xh, r), 4), "psnr_x_oracle_db": round(O.psnr(xh, r_ref), 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-layer HBM bytes per launch from the rocprofv3 PMC pass")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from neural_network_image_compression_amd import weights as W
+    from neural_network_image_compression_amd.codec import Codec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+        weights = broadcast_weights(W.seeded_weights(0) if rank == 0 else None, dist, rank, device)
+    else:
+        weights = W.seeded_weights(0)
+
+    B, S = args.batch, args.size
+    codec = Codec(local)
+    codec.set_weights(weights)
+    codec.reserve(B, S, S)
+    g = torch.Generator().manual_seed(1000 + rank)
+    x = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(device)
+    from neural_network_image_compression_amd._lib import latent_shape
+    h8, w8 = latent_shape(S, S)
+    z = torch.empty((B, h8, w8, 96), dtype=torch.uint8, device=device)
+    r = torch.empty((B, 8 * h8, 8 * w8, 3), dtype=torch.uint8, device=device)
+
+    def step():
+        codec.encode(x, out=z)
+        codec.decode(z, out=r)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # headline: K steps, barrier + sync on both sides, max over ranks
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # per-layer device time: hipEvents around every launch on the launch stream
+    codec.set_timing(True)
+    barrier()
+    for _ in range(args.steps):
+        step()
+    lt = codec.layer_times()
+    codec.set_timing(False)
+    torch.cuda.synchronize()
+
+    if rank != 0:
+        barrier()
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    P = 3 * B
+    geo = layer_geometry(S, S)
+    layers = {}
+    for name, (ms, n) in lt.items():
+        avg = ms / max(n, 1)
+        flop = geo[name] * P
+        layers[name] = {"avg_ms": round(avg, 4), "gflop_per_launch": round(flop / 1e9, 3),
+                        "tflops": round(flop / (avg * 1e-3) / 1e12, 2) if avg > 0 else None}
+    dom = max(layers, key=lambda k: layers[k]["avg_ms"])
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("batch") == B and tj.get("size") == S:
+                traffic = tj["layers"].get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    achieved = layers[dom]["tflops"]
+    roofline = {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "flop_per_launch": geo[dom] * P, "avg_launch_ms": layers[dom]["avg_ms"]}
+    total_flop = sum(geo.values()) * P
+    ms_step = el / args.steps * 1e3
+    value = world * B * S * S * args.steps / 1e6 / el
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"config2: {B}x{S}x{S}x3 u8 synthetic per GPU, encode+decode (torch seed 1000+rank)",
+                   "global_batch": world * B, "image": [S, S, 3], "parallelism": f"dp{world}",
+                   "weights": "seeded spread init (no trained checkpoint exists)"},
+        "step_tflops": round(total_flop / (ms_step * 1e-3) / 1e12, 2),
+        "step_frac_fp32_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+        "roofline": roofline, "layers": layers,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(weights, S, args.cpu_seconds)
+    if not args.no_parity:
+        out["parity"] = parity_sample(codec, x[:1], weights)
+    print(json.dumps(out), flush=True)
+    barrier()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+/*
+ * nic.h -- C-ABI of the MI355X-native learned-image-codec hot path.
+ *
+ * Drop-in boundary for the reference's TF2 codec surface
+ * (AlexFuster/Neural_network_image_compression, tf2_0/src):
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  -----------------------------------------
+ *   Encoder()/Decoder() + ProClass.load(path)   nic_create + nic_set_weights
+ *     encoder.py:34-36, decoder.py:35-37,
+ *     utils.py:15-17, 26-28
+ *   Encoder.__call__(x) encoder.py:38-47        nic_encode
+ *   Decoder.__call__(z) decoder.py:39-48        nic_decode
+ *   ProClass._feed_batch pack/unpack            nic_pack_latent / nic_unpack_latent
+ *     utils.py:35-36, 39-40
+ *   disc_entropy tf1_13/src/training.py:66-71   nic_entropy_hist
+ *
+ * Conventions
+ *  - Every buffer argument is a DEVICE pointer owned by the caller (e.g. a torch-ROCm
+ *    tensor's data_ptr()); inputs are never written.  The library owns only the weights
+ *    and a scratch workspace inside the nic_ctx, grown on demand (call nic_reserve to
+ *    size it ahead so no allocation happens in a timed or graph-captured call).
+ *  - Work is enqueued asynchronously on the caller's hipStream_t (NULL = default
+ *    stream).  One nic_ctx must not be used by two threads at once; distinct contexts
+ *    are independent.  There is no global mutable state besides the per-thread error.
+ *  - Layouts are NHWC uint8: images (N, H, W, 3); latents (N, ceil(H/8), ceil(W/8), 96)
+ *    with channels Y0..31, Cb0..31, Cr0..31 (encoder.py:45).  Sizes need not be multiples
+ *    of 8: like the reference, decode returns (N, 8h, 8w, 3).
+ *  - Return 0 on success or a negative NIC_E* code; nic_last_error() describes the most
+ *    recent failure on the calling thread.
+ */
+#ifndef NIC_H_
+#define NIC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nic_ctx nic_ctx;
+
+enum {
+  NIC_OK = 0,
+  NIC_EINVAL = -1,      /* null pointer, bad enum, bad layer name          */
+  NIC_ESHAPE = -2,      /* tensor shape does not match the architecture    */
+  NIC_ENOWEIGHTS = -3,  /* encode/decode before every tensor was set       */
+  NIC_EHIP = -4,        /* HIP runtime error                               */
+  NIC_ENOMEM = -5       /* device allocation failed                        */
+};
+
+/* model_id values for nic_set_weights (checkpoint names encoder{Y,CbCr}, decoder{Y,CbCr},
+ * training.py:167-172) */
+enum {
+  NIC_MODEL_ENCODER_Y = 0,
+  NIC_MODEL_ENCODER_CBCR = 1,
+  NIC_MODEL_DECODER_Y = 2,
+  NIC_MODEL_DECODER_CBCR = 3
+};
+
+/* ABI version: major * 10000 + minor * 100 + patch */
+int nic_version(void);
+
+/* Host copies of the fp32 colour constants the device uses: fp32(ycbcr_kernel) (utils.py:7),
+ * fp32(inv(ycbcr_kernel)) computed in float64 (utils.py:8), fp32(ycbcr_off) (utils.py:9).
+ * Row-major 3x3; any pointer may be NULL. */
+int nic_constants(float* ycbcr9, float* ycbcr_inv9, float* off3);
+
+/* Human-readable description of the last error on this thread ("" if none). */
+const char* nic_last_error(void);
+
+/* Create a context on HIP device `device`. */
+int nic_create(int device, nic_ctx** out);
+int nic_destroy(nic_ctx* ctx);
+
+/* Upload one tensor in its Keras layout from HOST memory (fp32, C order).
+ *   layer: "conv1".."conv8" (Conv2D kernel (kh,kw,Cin,Cout), encoder.py:10-17) or
+ *          "dconv1".."dconv8" (Conv2DTranspose kernel (kh,kw,Cout,Cin), decoder.py:10-17),
+ *          followed by "/kernel" or "/bias" (bias shape (Cout,)).
+ * The kernel is repacked to the device-native fragment layout.  Synchronous. */
+int nic_set_weights(nic_ctx* ctx, int model_id, const char* layer, const float* host, const int64_t* shape,
+                    int ndim);
+
+/* 1 when every tensor of the encoder pair (resp. decoder pair) has been set. */
+int nic_weights_ready(nic_ctx* ctx, int* encoder_ready, int* decoder_ready);
+
+/* Grow the workspace so encode of (n, h, w) images and decode of their latents allocate
+ * nothing.  Synchronous. */
+int nic_reserve(nic_ctx* ctx, int n, int h, int w);
+
+/* Latent spatial size for an h x w image: ceil(h/8), ceil(w/8) (TF SAME, three s2 convs). */
+int nic_latent_shape(int h, int w, int* h8, int* w8);
+
+/* Encoder.__call__: rgb (n,h,w,3) u8 -> latent (n,h8,w8,96) u8.
+ * prequant (nullable): (n,h8,w8,96) fp32, the clipped encoder output before round(x*255). */
+int nic_encode(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, float* prequant,
+               void* stream);
+
+/* Decoder.__call__: latent (n,h8,w8,96) u8 -> rgb (n,8*h8,8*w8,3) u8.
+ * rgb_f32 (nullable): the clipped fp32 RGB before round(x*255). */
+int nic_decode(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
+               void* stream);
+
+/* Histogram entropy of each latent plane (tf1_13/src/training.py:66-71).
+ * Plane order is the reference's concat along the batch: row p = plane p/n (Y,Cb,Cr) of
+ * image p%n.  counts (nullable): (3n, 256) uint32.  bits (nullable): (3n,) fp32
+ * bits/symbol.  Needs a ctx only for its scratch. */
+int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,
+                     void* stream);
+
+/* Bitstream image layout of ProClass._feed_batch: (n,h8,w8,96) <-> (n,4*h8,8*w8,3), each
+ * plane a raw C-order reshape (utils.py:35-36, 39-40). */
+int nic_pack_latent(const uint8_t* latent, int n, int h8, int w8, uint8_t* packed, void* stream);
+int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* latent, void* stream);
+
+/* Per-layer device timing.  With timing on, every kernel launch of encode/decode is
+ * bracketed by a hipEvent pair on the caller's stream (the stream the kernel runs on);
+ * nic_layer_times returns, per layer in the order conv1, conv2, conv3, conv4, conv8,
+ * dconv1, dconv5, dconv6, dconv7, dconv8 (NIC_LAYER_COUNT entries), the summed
+ * milliseconds and launch counts since timing was (re)enabled.  Both synchronise on
+ * the recorded events. */
+#define NIC_LAYER_COUNT 10
+int nic_set_timing(nic_ctx* ctx, int enable);
+int nic_layer_times(nic_ctx* ctx, double* ms_sum, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NIC_H_ */

@@ -1,0 +1,242 @@
+"""Host-side mirror of the reference codec surface, running on the HIP C-ABI.
+
+Reference classes (AlexFuster/Neural_network_image_compression, tf2_0/src):
+
+* ``ProClass`` (utils.py:15-62): owns the Y and CbCr models, ``load(path)`` reads
+  ``path + 'Y'`` and ``path + 'CbCr'``, ``_use_model``/``_feed_batch`` drive directories.
+* ``Encoder`` (encoder.py:34-51): ``__call__(x)`` u8 (N,H,W,3) -> u8 (N,h,w,96);
+  ``compress(dataset_path, checkpoint_path)``.
+* ``Decoder`` (decoder.py:35-52): ``__call__(z)`` u8 (N,h,w,96) -> u8 (N,8h,8w,3);
+  ``uncompress(dataset_path, checkpoint_path)``.
+
+Here the per-plane Keras models become one fused device pipeline over all 3N planes
+(``libnic.so``).  ``__call__`` accepts NumPy arrays (copied to and from the device, like
+the reference's ``.numpy()`` hand-offs) or ROCm ``torch.uint8`` tensors (no host copy;
+work is queued on the current torch stream and a device tensor is returned).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from . import weights as W
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _stream_ptr(torch, device: int) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _as_u8_array(x, what: str) -> np.ndarray:
+    a = np.asarray(x)
+    if a.dtype == np.uint8:
+        return a
+    if a.dtype.kind in "iuf":
+        # the reference computes x.astype(float32)/255 (encoder.py:39, decoder.py:40); the
+        # device path is defined on u8 codes, so only exactly representable inputs are taken
+        if a.size and (not np.all(np.isfinite(a)) or np.any(a != np.round(a)) or a.min() < 0 or a.max() > 255):
+            raise ValueError(f"{what}: values must be integers in [0, 255], got dtype {a.dtype}")
+        return a.astype(np.uint8)
+    raise TypeError(f"{what}: unsupported dtype {a.dtype}")
+
+
+class Codec:
+    """One ``nic_ctx`` on one HIP device: weights + workspace for encode/decode/entropy."""
+
+    def __init__(self, device: Optional[int] = None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("neural_network_image_compression_amd needs a ROCm GPU (no CPU fallback)")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self._L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(self._L.nic_create(self.device, ctypes.byref(h)), "nic_create")
+        self._h = h
+        self._keep: Dict[str, np.ndarray] = {}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.nic_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- weights ---------------------------------------------------------------------
+    def set_tensor(self, model: str, layer: str, kind: str, value: np.ndarray) -> None:
+        a = np.ascontiguousarray(value, dtype=np.float32)
+        shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+        rc = self._L.nic_set_weights(self._h, W.MODEL_ID[model], f"{layer}/{kind}".encode(), a.ctypes.data,
+                                     shape, a.ndim)
+        _lib.check(rc, f"nic_set_weights({model}/{layer}/{kind})")
+
+    def set_weights(self, weights: W.Weights) -> None:
+        for key, value in weights.items():
+            model, layer, kind = key.split("/")
+            if model not in W.MODEL_ID:
+                raise KeyError(f"unknown model {model!r} in key {key!r}")
+            self.set_tensor(model, layer, kind, value)
+
+    def ready(self):
+        e, d = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self._L.nic_weights_ready(self._h, ctypes.byref(e), ctypes.byref(d)), "nic_weights_ready")
+        return bool(e.value), bool(d.value)
+
+    def set_timing(self, enable: bool) -> None:
+        """Bracket every layer launch with hipEvents on the launch stream (resets the sums)."""
+        _lib.check(self._L.nic_set_timing(self._h, int(bool(enable))), "nic_set_timing")
+
+    def layer_times(self):
+        """{layer: (total_ms, launches)} accumulated since set_timing(True)."""
+        ms = np.zeros(len(_lib.LAYER_NAMES), np.float64)
+        cnt = np.zeros(len(_lib.LAYER_NAMES), np.int64)
+        _lib.check(self._L.nic_layer_times(self._h, ms.ctypes.data, cnt.ctypes.data), "nic_layer_times")
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(_lib.LAYER_NAMES)}
+
+    def reserve(self, n: int, h: int, w: int) -> None:
+        _lib.check(self._L.nic_reserve(self._h, n, h, w), "nic_reserve")
+
+    # -- device entry points (torch uint8 tensors on this device) ----------------------
+    def _check_dev(self, t, ndim: int, last: int, what: str):
+        torch = _torch()
+        if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or t.device.type != "cuda":
+            raise TypeError(f"{what}: expected a cuda torch.uint8 tensor")
+        if t.device.index != self.device:
+            raise ValueError(f"{what}: tensor on cuda:{t.device.index}, codec on cuda:{self.device}")
+        if t.ndim != ndim or t.shape[-1] != last:
+            raise ValueError(f"{what}: expected shape (N,H,W,{last}), got {tuple(t.shape)}")
+        return t.contiguous()
+
+    def encode(self, x, prequant: bool = False, out=None):
+        """(N,H,W,3) u8 -> (N,ceil(H/8),ceil(W/8),96) u8 [, fp32 clipped pre-quant latent]."""
+        torch = _torch()
+        x = self._check_dev(x, 4, 3, "encode")
+        n, h, w, _ = x.shape
+        h8, w8 = _lib.latent_shape(h, w)
+        z = out if out is not None else torch.empty((n, h8, w8, 96), dtype=torch.uint8, device=x.device)
+        f = torch.empty((n, h8, w8, 96), dtype=torch.float32, device=x.device) if prequant else None
+        rc = self._L.nic_encode(self._h, x.data_ptr(), n, h, w, z.data_ptr(), f.data_ptr() if f is not None else None,
+                                _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_encode")
+        return (z, f) if prequant else z
+
+    def decode(self, z, rgb_f32: bool = False, out=None):
+        """(N,h,w,96) u8 -> (N,8h,8w,3) u8 [, fp32 clipped RGB before quantisation]."""
+        torch = _torch()
+        z = self._check_dev(z, 4, 96, "decode")
+        n, h8, w8, _ = z.shape
+        x = out if out is not None else torch.empty((n, 8 * h8, 8 * w8, 3), dtype=torch.uint8, device=z.device)
+        f = torch.empty((n, 8 * h8, 8 * w8, 3), dtype=torch.float32, device=z.device) if rgb_f32 else None
+        rc = self._L.nic_decode(self._h, z.data_ptr(), n, h8, w8, x.data_ptr(), f.data_ptr() if f is not None else None,
+                                _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_decode")
+        return (x, f) if rgb_f32 else x
+
+    def entropy(self, z, counts: bool = False):
+        """Histogram entropy per latent plane: (3N,) fp32 bits/symbol [, (3N,256) int32 counts]."""
+        torch = _torch()
+        z = self._check_dev(z, 4, 96, "entropy")
+        n, h8, w8, _ = z.shape
+        bits = torch.empty((3 * n,), dtype=torch.float32, device=z.device)
+        cnt = torch.empty((3 * n, 256), dtype=torch.int32, device=z.device) if counts else None
+        rc = self._L.nic_entropy_hist(self._h, z.data_ptr(), n, h8, w8, cnt.data_ptr() if cnt is not None else None,
+                                      bits.data_ptr(), _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_entropy_hist")
+        return (bits, cnt) if counts else bits
+
+    def pack(self, z):
+        """(N,h,w,96) -> (N,4h,8w,3) bitstream image (utils.py:39-40)."""
+        torch = _torch()
+        z = self._check_dev(z, 4, 96, "pack")
+        n, h8, w8, _ = z.shape
+        out = torch.empty((n, 4 * h8, 8 * w8, 3), dtype=torch.uint8, device=z.device)
+        _lib.check(self._L.nic_pack_latent(z.data_ptr(), n, h8, w8, out.data_ptr(), _stream_ptr(torch, self.device)),
+                   "nic_pack_latent")
+        return out
+
+    def unpack(self, img):
+        """(N,4h,8w,3) -> (N,h,w,96) (utils.py:35-36)."""
+        torch = _torch()
+        img = self._check_dev(img, 4, 3, "unpack")
+        n, hh, ww, _ = img.shape
+        if hh % 4 or ww % 8:
+            raise ValueError(f"unpack: packed image {tuple(img.shape)} is not (N,4h,8w,3)")
+        out = torch.empty((n, hh // 4, ww // 8, 96), dtype=torch.uint8, device=img.device)
+        _lib.check(self._L.nic_unpack_latent(img.data_ptr(), n, hh // 4, ww // 8, out.data_ptr(),
+                                             _stream_ptr(torch, self.device)), "nic_unpack_latent")
+        return out
+
+
+class ProClass:
+    """utils.py:15-62: shared Y/CbCr model holder (kind 'encoder' or 'decoder')."""
+
+    kind = ""
+
+    def __init__(self, device: Optional[int] = None, codec: Optional[Codec] = None):
+        self.codec = codec if codec is not None else Codec(device)
+
+    def load(self, path: str) -> None:
+        """utils.py:26-28: weights from ``path + 'Y'`` and ``path + 'CbCr'`` (safetensors)."""
+        self.codec.set_weights(W.load(path, self.kind))
+
+    def set_weights(self, weights: W.Weights) -> None:
+        sub = {k: v for k, v in weights.items() if k.startswith(self.kind)}
+        W.validate(sub, [self.kind + m for m in W.PLANE_MODELS])
+        self.codec.set_weights(sub)
+
+    def _device_call(self, x):
+        raise NotImplementedError
+
+    def __call__(self, x):
+        torch = _torch()
+        if isinstance(x, torch.Tensor) and x.device.type == "cuda":
+            return self._device_call(x)
+        a = _as_u8_array(x.cpu().numpy() if isinstance(x, torch.Tensor) else x, type(self).__name__)
+        if a.ndim != 4:
+            raise ValueError(f"{type(self).__name__}: expected a 4-D NHWC batch, got shape {a.shape}")
+        dev = torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{self.codec.device}")
+        out = self._device_call(dev)
+        return out.cpu().numpy()
+
+
+class Encoder(ProClass):
+    """encoder.py:34-51."""
+
+    kind = "encoder"
+
+    def _device_call(self, x):
+        return self.codec.encode(x)
+
+    def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4) -> None:
+        """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``."""
+        from .bitstream import use_model
+
+        use_model(self, dataset_path, checkpoint_path, dataset_path + "_compressed", in_cshape=3,
+                  batch_size=batch_size)
+
+
+class Decoder(ProClass):
+    """decoder.py:35-52."""
+
+    kind = "decoder"
+
+    def _device_call(self, z):
+        return self.codec.decode(z)
+
+    def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4) -> None:
+        """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``."""
+        from .bitstream import use_model
+
+        use_model(self, dataset_path, checkpoint_path, dataset_path.replace("compressed", "uncompressed"),
+                  in_cshape=96, batch_size=batch_size)

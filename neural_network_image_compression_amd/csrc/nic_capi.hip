@@ -1,0 +1,618 @@
+// C-ABI of the codec hot path (declared in include/nic.h): context, Keras-layout weight
+// upload + repack to the kernels' fragment layouts, and the encode / decode pipelines.
+//
+// Pipeline per call (P = 3N planes, Y planes first, then Cb, then Cr):
+//   encode: conv1+colour (rgb u8 -> R0) -> conv2 (R0 -> R1) -> conv3 (R1 -> R2)
+//           -> conv4 + res (R2, R1 -> R3) -> conv8 + clip + quantise (R3 -> latent u8)
+//   decode: dconv1 + dequantise (latent u8 -> R1) -> dconv5 (R1 -> R2)
+//           -> dconv6 + res (R2, R1 -> R3) -> dconv7 (R3 -> R0)
+//           -> dconv8 + inverse colour + quantise (R0 -> rgb u8)
+// mirroring BaseEncoder.call (encoder.py:19-32) / BaseDecoder.call (decoder.py:19-32).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nic.h"
+#include "nic_kernels.h"
+
+using namespace nic;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) return fail(NIC_EHIP, "%s: %s", #expr, hipGetErrorString(_e));     \
+  } while (0)
+
+struct LayerSpec {
+  const char* name;
+  int k, s, cin, cout;
+  bool transposed;
+  LayerId id;
+};
+
+// encoder.py:10-17, decoder.py:10-17
+const LayerSpec kEnc[5] = {
+    {"conv1", 5, 2, 1, 32, false, L_CONV1},  {"conv2", 5, 2, 32, 64, false, L_CONV2},
+    {"conv3", 3, 1, 64, 64, false, L_CONV3}, {"conv4", 3, 1, 64, 64, false, L_CONV4},
+    {"conv8", 5, 2, 64, 32, false, L_CONV8},
+};
+const LayerSpec kDec[5] = {
+    {"dconv1", 5, 2, 32, 64, true, L_DCONV1}, {"dconv5", 3, 1, 64, 64, true, L_DCONV5},
+    {"dconv6", 3, 1, 64, 64, true, L_DCONV6}, {"dconv7", 5, 2, 64, 64, true, L_DCONV7},
+    {"dconv8", 5, 2, 64, 1, true, L_DCONV8},
+};
+
+// device floats per model for a layer's repacked kernel
+size_t packed_kernel_floats(const LayerSpec& L) {
+  if (L.id == L_CONV1) return 26 * 32;
+  if (L.id == L_DCONV8) return 25 * 64;
+  return (size_t)L.k * L.k * L.cin * L.cout;
+}
+
+// Forward-conv fragment order: Wr[tap][q][h][co][r] with ci = 8q + 4h + r.
+// get(tap, ci, co) returns the weight multiplying input channel ci for output co at tap.
+template <class F>
+void repack_fragments(std::vector<float>& out, int taps, int cin, int cout, F get) {
+  out.assign((size_t)taps * cin * cout, 0.f);
+  for (int t = 0; t < taps; ++t)
+    for (int q = 0; q < cin / 8; ++q)
+      for (int h = 0; h < 2; ++h)
+        for (int co = 0; co < cout; ++co)
+          for (int r = 0; r < 4; ++r) {
+            const int ci = 8 * q + 4 * h + r;
+            out[((((size_t)t * (cin / 8) + q) * 2 + h) * cout + co) * 4 + r] = get(t, ci, co);
+          }
+}
+
+// Phase-major tap enumeration of a k5 s2 Conv2DTranspose: for phase (py, px) and
+// halo offsets (iy, ix), the kernel tap is (py + 3 - 2*iy, px + 3 - 2*ix).
+template <class F>
+void for_each_phase_tap(F f) {
+  int t = 0;
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1, ny = py ? 3 : 2, nx = px ? 3 : 2;
+    for (int iy = 0; iy < ny; ++iy)
+      for (int ix = 0; ix < nx; ++ix) f(t++, py + 3 - 2 * iy, px + 3 - 2 * ix);
+  }
+}
+
+void repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out) {
+  const int k = L.k, cin = L.cin, cout = L.cout;
+  if (L.id == L_CONV1) {  // HWIO (5,5,1,32) -> [26][32], tap 25 = 0
+    out.assign(26 * 32, 0.f);
+    for (int t = 0; t < 25; ++t)
+      for (int co = 0; co < 32; ++co) out[t * 32 + co] = K[t * 32 + co];
+  } else if (L.id == L_DCONV8) {  // (5,5,1,64) (kh,kw,Cout,Cin) -> [25 phase taps][64]
+    out.assign(25 * 64, 0.f);
+    for_each_phase_tap([&](int t, int ky, int kx) {
+      for (int ci = 0; ci < 64; ++ci) out[t * 64 + ci] = K[((size_t)(ky * 5 + kx) * 1 + 0) * 64 + ci];
+    });
+  } else if (!L.transposed) {  // HWIO
+    repack_fragments(out, k * k, cin, cout,
+                     [&](int t, int ci, int co) { return K[((size_t)t * cin + ci) * cout + co]; });
+  } else if (L.s == 1) {  // transposed k3 s1 == conv with flipped taps, swapped channels
+    repack_fragments(out, k * k, cin, cout, [&](int t, int ci, int co) {
+      const int u = t / k, v = t % k;
+      const int ky = k - 1 - u, kx = k - 1 - v;
+      return K[(((size_t)ky * k + kx) * cout + co) * cin + ci];
+    });
+  } else {  // transposed k5 s2, phase-major taps
+    std::vector<int> tap_ky(25), tap_kx(25);
+    for_each_phase_tap([&](int t, int ky, int kx) {
+      tap_ky[t] = ky;
+      tap_kx[t] = kx;
+    });
+    repack_fragments(out, 25, cin, cout, [&](int t, int ci, int co) {
+      return K[(((size_t)tap_ky[t] * 5 + tap_kx[t]) * cout + co) * cin + ci];
+    });
+  }
+}
+
+struct SamePad {
+  int out, lo;
+};
+SamePad same_pad(int n, int k, int s) {
+  const int out = (n + s - 1) / s;
+  const int pad = std::max((out - 1) * s + k - n, 0);
+  return {out, pad / 2};
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct nic_ctx {
+  int device = 0;
+  float* wk[L_COUNT] = {};  // [2 models][packed kernel]
+  float* wb[L_COUNT] = {};  // [2 models][cout]
+  bool have_k[4][5] = {};
+  bool have_b[4][5] = {};
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  uint32_t* counts = nullptr;
+  size_t counts_bytes = 0;
+  // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
+  // call, read back and accumulated by nic_layer_times
+  bool timing = false;
+  hipEvent_t ev[L_COUNT][2] = {};
+  bool ev_pending[L_COUNT] = {};
+  double ms_sum[L_COUNT] = {};
+  long launches[L_COUNT] = {};
+};
+
+namespace {
+
+const LayerSpec* find_layer(int model_id, const char* name, int* index) {
+  const LayerSpec* tab = model_id < 2 ? kEnc : kDec;
+  for (int i = 0; i < 5; ++i)
+    if (std::strcmp(tab[i].name, name) == 0) {
+      *index = i;
+      return &tab[i];
+    }
+  return nullptr;
+}
+
+int ensure_ws(nic_ctx* c, size_t bytes) {
+  if (bytes <= c->ws_bytes) return NIC_OK;
+  if (c->ws) HIP_TRY(hipFree(c->ws));
+  c->ws = nullptr;
+  c->ws_bytes = 0;
+  if (hipMalloc(&c->ws, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(NIC_ENOMEM, "workspace allocation of %zu bytes failed", bytes);
+  }
+  c->ws_bytes = bytes;
+  return NIC_OK;
+}
+
+struct EncGeom {
+  SamePad c1y, c1x, c2y, c2x, c8y, c8x;
+  size_t r0, r123;  // floats per region
+};
+EncGeom enc_geom(int n, int h, int w) {
+  EncGeom g;
+  g.c1y = same_pad(h, 5, 2);
+  g.c1x = same_pad(w, 5, 2);
+  g.c2y = same_pad(g.c1y.out, 5, 2);
+  g.c2x = same_pad(g.c1x.out, 5, 2);
+  g.c8y = same_pad(g.c2y.out, 5, 2);
+  g.c8x = same_pad(g.c2x.out, 5, 2);
+  const size_t P = 3 * (size_t)n;
+  g.r0 = P * g.c1y.out * g.c1x.out * 32;
+  g.r123 = P * g.c2y.out * g.c2x.out * 64;
+  return g;
+}
+struct DecGeom {
+  size_t r0, r123;
+};
+DecGeom dec_geom(int n, int h8, int w8) {
+  const size_t P = 3 * (size_t)n;
+  return {P * (4 * (size_t)h8) * (4 * (size_t)w8) * 64, P * (2 * (size_t)h8) * (2 * (size_t)w8) * 64};
+}
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int ensure_regions(nic_ctx* c, size_t r0, size_t r123, float** R) {
+  const size_t b0 = align_up(r0 * 4), b1 = align_up(r123 * 4);
+  int rc = ensure_ws(c, b0 + 3 * b1);
+  if (rc) return rc;
+  R[0] = (float*)c->ws;
+  R[1] = (float*)(c->ws + b0);
+  R[2] = (float*)(c->ws + b0 + b1);
+  R[3] = (float*)(c->ws + b0 + 2 * b1);
+  return NIC_OK;
+}
+
+// Collect a finished event pair of layer id into the running sums.
+int collect_layer(nic_ctx* c, int id) {
+  if (!c->ev_pending[id]) return NIC_OK;
+  HIP_TRY(hipEventSynchronize(c->ev[id][1]));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev[id][0], c->ev[id][1]));
+  c->ms_sum[id] += ms;
+  c->launches[id] += 1;
+  c->ev_pending[id] = false;
+  return NIC_OK;
+}
+
+// Bracket one launch with the layer's event pair when timing is on.
+struct LayerTimer {
+  nic_ctx* c;
+  int id;
+  hipStream_t st;
+  int rc = NIC_OK;
+  LayerTimer(nic_ctx* c_, int id_, hipStream_t st_) : c(c_), id(id_), st(st_) {
+    if (!c->timing) return;
+    rc = collect_layer(c, id);  // previous call's pair must be read before reuse
+    if (rc == NIC_OK && hipEventRecord(c->ev[id][0], st) != hipSuccess) rc = fail(NIC_EHIP, "hipEventRecord");
+  }
+  int done() {
+    if (!c->timing || rc) return rc;
+    if (hipEventRecord(c->ev[id][1], st) != hipSuccess) return fail(NIC_EHIP, "hipEventRecord");
+    c->ev_pending[id] = true;
+    return NIC_OK;
+  }
+};
+
+#define TIMED(layer, launch_expr)                  \
+  do {                                             \
+    LayerTimer _t(c, layer, st);                   \
+    if (_t.rc) return _t.rc;                       \
+    HIP_TRY(launch_expr);                          \
+    int _rc = _t.done();                           \
+    if (_rc) return _rc;                           \
+  } while (0)
+
+bool models_ready(const nic_ctx* c, int m0) {
+  for (int m = m0; m < m0 + 2; ++m)
+    for (int i = 0; i < 5; ++i)
+      if (!c->have_k[m][i] || !c->have_b[m][i]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nic_version(void) { return 100; }
+
+int nic_constants(float* ycbcr9, float* ycbcr_inv9, float* off3) {
+  // host copy of what nic_create uploads; lets tests compare with np.linalg.inv (utils.py:8)
+  const double K[9] = {0.299, 0.587, 0.114, -0.16874, -0.33126, 0.5, 0.5, -0.41869, -0.08131};
+  const double det = K[0] * (K[4] * K[8] - K[5] * K[7]) - K[1] * (K[3] * K[8] - K[5] * K[6]) +
+                     K[2] * (K[3] * K[7] - K[4] * K[6]);
+  const double inv[9] = {(K[4] * K[8] - K[5] * K[7]) / det, (K[2] * K[7] - K[1] * K[8]) / det,
+                         (K[1] * K[5] - K[2] * K[4]) / det, (K[5] * K[6] - K[3] * K[8]) / det,
+                         (K[0] * K[8] - K[2] * K[6]) / det, (K[2] * K[3] - K[0] * K[5]) / det,
+                         (K[3] * K[7] - K[4] * K[6]) / det, (K[1] * K[6] - K[0] * K[7]) / det,
+                         (K[0] * K[4] - K[1] * K[3]) / det};
+  for (int i = 0; i < 9; ++i) {
+    if (ycbcr9) ycbcr9[i] = (float)K[i];
+    if (ycbcr_inv9) ycbcr_inv9[i] = (float)inv[i];
+  }
+  if (off3) {
+    off3[0] = 0.0f;
+    off3[1] = 0.5f;
+    off3[2] = 0.5f;
+  }
+  return NIC_OK;
+}
+
+const char* nic_last_error(void) { return g_err.c_str(); }
+
+int nic_create(int device, nic_ctx** out) {
+  if (!out) return fail(NIC_EINVAL, "nic_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(NIC_EINVAL, "nic_create: device %d out of range [0,%d)", device, ndev);
+  DeviceGuard guard(device);
+  nic_ctx* c = new nic_ctx();
+  c->device = device;
+  for (int half = 0; half < 2; ++half) {
+    const LayerSpec* tab = half ? kDec : kEnc;
+    for (int i = 0; i < 5; ++i) {
+      const LayerSpec& L = tab[i];
+      const size_t kb = 2 * packed_kernel_floats(L) * sizeof(float), bb = 2 * L.cout * sizeof(float);
+      if (hipMalloc(&c->wk[L.id], kb) != hipSuccess || hipMalloc(&c->wb[L.id], bb) != hipSuccess) {
+        nic_destroy(c);
+        return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
+      }
+      (void)hipMemset(c->wk[L.id], 0, kb);
+      (void)hipMemset(c->wb[L.id], 0, bb);
+    }
+  }
+  // constants: u8 -> fp32 /255 (correctly rounded on the host), colour matrices
+  // (utils.py:7-9; the inverse is np.linalg.inv in float64, then rounded to fp32)
+  float lut[256];
+  for (int i = 0; i < 256; ++i) lut[i] = (float)i / 255.0f;
+  float kf[9], kinv[9], off[3];
+  nic_constants(kf, kinv, off);
+  hipError_t e = upload_constants(lut, kf, kinv, off);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    nic_destroy(c);
+    return fail(NIC_EHIP, "nic_create: constant upload: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return NIC_OK;
+}
+
+int nic_destroy(nic_ctx* c) {
+  if (!c) return NIC_OK;
+  DeviceGuard guard(c->device);
+  for (int i = 0; i < L_COUNT; ++i) {
+    if (c->wk[i]) (void)hipFree(c->wk[i]);
+    if (c->wb[i]) (void)hipFree(c->wb[i]);
+  }
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->counts) (void)hipFree(c->counts);
+  for (int i = 0; i < L_COUNT; ++i)
+    for (int j = 0; j < 2; ++j)
+      if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
+  delete c;
+  return NIC_OK;
+}
+
+int nic_set_weights(nic_ctx* c, int model_id, const char* layer, const float* host, const int64_t* shape,
+                    int ndim) {
+  if (!c || !layer || !host || !shape) return fail(NIC_EINVAL, "nic_set_weights: NULL argument");
+  if (model_id < 0 || model_id > 3) return fail(NIC_EINVAL, "nic_set_weights: model_id %d not in 0..3", model_id);
+  const char* slash = std::strchr(layer, '/');
+  if (!slash) return fail(NIC_EINVAL, "nic_set_weights: layer '%s' must be '<name>/kernel' or '<name>/bias'", layer);
+  const std::string lname(layer, slash - layer), kind(slash + 1);
+  int idx = -1;
+  const LayerSpec* L = find_layer(model_id, lname.c_str(), &idx);
+  if (!L) return fail(NIC_EINVAL, "nic_set_weights: model %d has no layer '%s'", model_id, lname.c_str());
+  const int m = model_id & 1;  // slot within the encoder / decoder pair
+  DeviceGuard guard(c->device);
+  if (kind == "kernel") {
+    const int64_t want[4] = {L->k, L->k, L->transposed ? L->cout : L->cin, L->transposed ? L->cin : L->cout};
+    if (ndim != 4 || shape[0] != want[0] || shape[1] != want[1] || shape[2] != want[2] || shape[3] != want[3])
+      return fail(NIC_ESHAPE, "nic_set_weights: %s/kernel expects shape (%lld,%lld,%lld,%lld)", lname.c_str(),
+                  (long long)want[0], (long long)want[1], (long long)want[2], (long long)want[3]);
+    std::vector<float> packed;
+    repack_kernel(*L, host, packed);
+    HIP_TRY(hipMemcpy(c->wk[L->id] + m * packed.size(), packed.data(), packed.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    c->have_k[model_id][idx] = true;
+  } else if (kind == "bias") {
+    if (ndim != 1 || shape[0] != L->cout)
+      return fail(NIC_ESHAPE, "nic_set_weights: %s/bias expects shape (%d,)", lname.c_str(), L->cout);
+    HIP_TRY(hipMemcpy(c->wb[L->id] + m * L->cout, host, L->cout * sizeof(float), hipMemcpyHostToDevice));
+    c->have_b[model_id][idx] = true;
+  } else {
+    return fail(NIC_EINVAL, "nic_set_weights: '%s' is neither kernel nor bias", kind.c_str());
+  }
+  return NIC_OK;
+}
+
+int nic_weights_ready(nic_ctx* c, int* enc, int* dec) {
+  if (!c) return fail(NIC_EINVAL, "nic_weights_ready: NULL ctx");
+  if (enc) *enc = models_ready(c, 0);
+  if (dec) *dec = models_ready(c, 2);
+  return NIC_OK;
+}
+
+int nic_latent_shape(int h, int w, int* h8, int* w8) {
+  if (h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_latent_shape: h=%d w=%d must be positive", h, w);
+  const SamePad a = same_pad(same_pad(same_pad(h, 5, 2).out, 5, 2).out, 5, 2);
+  const SamePad b = same_pad(same_pad(same_pad(w, 5, 2).out, 5, 2).out, 5, 2);
+  if (h8) *h8 = a.out;
+  if (w8) *w8 = b.out;
+  return NIC_OK;
+}
+
+int nic_reserve(nic_ctx* c, int n, int h, int w) {
+  if (!c) return fail(NIC_EINVAL, "nic_reserve: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_reserve: bad shape (%d,%d,%d)", n, h, w);
+  DeviceGuard guard(c->device);
+  const EncGeom e = enc_geom(n, h, w);
+  const DecGeom d = dec_geom(n, e.c8y.out, e.c8x.out);
+  float* R[4];
+  int rc = ensure_regions(c, std::max(e.r0, d.r0), std::max(e.r123, d.r123), R);
+  if (rc) return rc;
+  const size_t cb = (size_t)3 * n * 256 * sizeof(uint32_t);
+  if (cb > c->counts_bytes) {
+    if (c->counts) HIP_TRY(hipFree(c->counts));
+    c->counts = nullptr;
+    c->counts_bytes = 0;
+    HIP_TRY(hipMalloc(&c->counts, cb));
+    c->counts_bytes = cb;
+  }
+  return NIC_OK;
+}
+
+int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, float* prequant,
+               void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_encode: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode: encoder weights not fully set");
+  if (n == 0) return NIC_OK;  // empty batch: pointers may be NULL
+  if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  const EncGeom g = enc_geom(n, h, w);
+  float* R[4];
+  int rc = ensure_regions(c, g.r0, g.r123, R);
+  if (rc) return rc;
+  const int P = 3 * n;
+
+  Conv1Args a1{};
+  a1.rgb = rgb;
+  a1.out = R[0];
+  a1.w = c->wk[L_CONV1];
+  a1.bias = c->wb[L_CONV1];
+  a1.P = P;
+  a1.nimg = n;
+  a1.H = h;
+  a1.W = w;
+  a1.OH = g.c1y.out;
+  a1.OW = g.c1x.out;
+  a1.pad_y = g.c1y.lo;
+  a1.pad_x = g.c1x.lo;
+  TIMED(L_CONV1, launch_conv1(a1, st));
+
+  auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW, int py,
+                  int px) {
+    ConvArgs a{};
+    a.in = in;
+    a.out = out;
+    a.res = res;
+    a.w = c->wk[id];
+    a.bias = c->wb[id];
+    a.P = P;
+    a.nimg = n;
+    a.H = H;
+    a.W = W;
+    a.OH = OH;
+    a.OW = OW;
+    a.pad_y = py;
+    a.pad_x = px;
+    return a;
+  };
+  const int h1 = g.c1y.out, w1 = g.c1x.out, h2 = g.c2y.out, w2 = g.c2x.out;
+  TIMED(L_CONV2, launch_layer(L_CONV2, conv(L_CONV2, R[0], R[1], nullptr, h1, w1, h2, w2, g.c2y.lo, g.c2x.lo), st));
+  TIMED(L_CONV3, launch_layer(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1), st));
+  TIMED(L_CONV4, launch_layer(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1), st));
+  ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);
+  a8.out_u8 = latent;
+  a8.out_f32_latent = prequant;
+  TIMED(L_CONV8, launch_layer(L_CONV8, a8, st));
+  return NIC_OK;
+}
+
+int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
+               void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_decode: NULL ctx");
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_decode: bad latent shape (%d,%d,%d,96)", n, h8, w8);
+  if (!models_ready(c, 2)) return fail(NIC_ENOWEIGHTS, "nic_decode: decoder weights not fully set");
+  if (n == 0) return NIC_OK;
+  if (!latent || !rgb) return fail(NIC_EINVAL, "nic_decode: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_decode: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  const DecGeom g = dec_geom(n, h8, w8);
+  float* R[4];
+  int rc = ensure_regions(c, g.r0, g.r123, R);
+  if (rc) return rc;
+  const int P = 3 * n;
+  auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW) {
+    ConvArgs a{};
+    a.in = in;
+    a.out = out;
+    a.res = res;
+    a.w = c->wk[id];
+    a.bias = c->wb[id];
+    a.P = P;
+    a.nimg = n;
+    a.H = H;
+    a.W = W;
+    a.OH = OH;
+    a.OW = OW;
+    a.pad_y = 1;
+    a.pad_x = 1;
+    return a;
+  };
+  ConvArgs d1 = conv(L_DCONV1, nullptr, R[1], nullptr, h8, w8, 2 * h8, 2 * w8);
+  d1.in_u8 = latent;
+  TIMED(L_DCONV1, launch_layer(L_DCONV1, d1, st));
+  const int h2 = 2 * h8, w2 = 2 * w8;
+  TIMED(L_DCONV5, launch_layer(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2), st));
+  TIMED(L_DCONV6, launch_layer(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2), st));
+  TIMED(L_DCONV7, launch_layer(L_DCONV7, conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2), st));
+  Dconv8Args a8{};
+  a8.in = R[0];
+  a8.out_u8 = rgb;
+  a8.out_f32 = rgb_f32;
+  a8.w = c->wk[L_DCONV8];
+  a8.bias = c->wb[L_DCONV8];
+  a8.nimg = n;
+  a8.H = 2 * h2;
+  a8.W = 2 * w2;
+  TIMED(L_DCONV8, launch_dconv8(a8, st));
+  return NIC_OK;
+}
+
+int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,
+                     void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_entropy_hist: NULL ctx");
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_entropy_hist: bad latent shape (%d,%d,%d,96)", n, h8, w8);
+  if (n == 0 || (!counts && !bits)) return NIC_OK;
+  if (!latent) return fail(NIC_EINVAL, "nic_entropy_hist: NULL latent");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_entropy_hist: batch %d too large", n);
+  DeviceGuard guard(c->device);
+  uint32_t* cnt = counts;
+  if (!cnt) {
+    const size_t cb = (size_t)3 * n * 256 * sizeof(uint32_t);
+    if (cb > c->counts_bytes) {
+      if (c->counts) HIP_TRY(hipFree(c->counts));
+      c->counts = nullptr;
+      c->counts_bytes = 0;
+      HIP_TRY(hipMalloc(&c->counts, cb));
+      c->counts_bytes = cb;
+    }
+    cnt = c->counts;
+  }
+  HIP_TRY(launch_hist(latent, n, h8 * w8, cnt, bits, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_pack_latent(const uint8_t* latent, int n, int h8, int w8, uint8_t* packed, void* stream) {
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_pack_latent: bad shape (%d,%d,%d)", n, h8, w8);
+  if (n == 0) return NIC_OK;
+  if (!latent || !packed) return fail(NIC_EINVAL, "nic_pack_latent: NULL argument");
+  HIP_TRY(launch_pack(latent, packed, n, h8, w8, false, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* latent, void* stream) {
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_unpack_latent: bad shape (%d,%d,%d)", n, h8, w8);
+  if (n == 0) return NIC_OK;
+  if (!latent || !packed) return fail(NIC_EINVAL, "nic_unpack_latent: NULL argument");
+  HIP_TRY(launch_pack(packed, latent, n, h8, w8, true, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_set_timing(nic_ctx* c, int enable) {
+  if (!c) return fail(NIC_EINVAL, "nic_set_timing: NULL ctx");
+  DeviceGuard guard(c->device);
+  if (enable && !c->ev[0][0]) {
+    for (int i = 0; i < L_COUNT; ++i)
+      for (int j = 0; j < 2; ++j) HIP_TRY(hipEventCreate(&c->ev[i][j]));
+  }
+  for (int i = 0; i < L_COUNT; ++i) {
+    int rc = collect_layer(c, i);
+    if (rc) return rc;
+    c->ms_sum[i] = 0.0;
+    c->launches[i] = 0;
+  }
+  c->timing = enable != 0;
+  return NIC_OK;
+}
+
+int nic_layer_times(nic_ctx* c, double* ms_sum, int64_t* launches) {
+  if (!c) return fail(NIC_EINVAL, "nic_layer_times: NULL ctx");
+  DeviceGuard guard(c->device);
+  for (int i = 0; i < L_COUNT; ++i) {
+    int rc = collect_layer(c, i);
+    if (rc) return rc;
+    if (ms_sum) ms_sum[i] = c->ms_sum[i];
+    if (launches) launches[i] = c->launches[i];
+  }
+  return NIC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,57 @@
+// Internal kernel interface (not part of the public C-ABI; see include/nic.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nic {
+
+enum InMode { IN_F32 = 0, IN_U8_LATENT = 1 };
+enum OutMode { OUT_F32 = 0, OUT_U8_LATENT = 1 };
+
+enum LayerId {
+  L_CONV1 = 0, L_CONV2, L_CONV3, L_CONV4, L_CONV8,
+  L_DCONV1, L_DCONV5, L_DCONV6, L_DCONV7, L_DCONV8,
+  L_COUNT
+};
+
+struct ConvArgs {
+  const float* in;        // [P][H][W][Cin] fp32 (IN_F32)
+  const uint8_t* in_u8;   // [N][H][W][96] latent (IN_U8_LATENT)
+  float* out;             // [P][OH][OW][Cout] fp32 (OUT_F32)
+  const float* res;       // residual, same layout as out
+  uint8_t* out_u8;        // [N][OH][OW][96] latent (OUT_U8_LATENT)
+  float* out_f32_latent;  // optional clipped fp32 latent, same layout as out_u8
+  const float* w;         // repacked weights [2 models][taps][Cin/8][2][Cout][4]
+  const float* bias;      // [2][Cout]
+  int P, nimg;            // planes (= 3 * nimg), images
+  int H, W;               // input spatial dims
+  int OH, OW;             // output spatial dims
+  int pad_y, pad_x;       // forward conv TF-SAME pad_lo
+  int tiles_x;            // set by the launcher
+};
+
+struct Conv1Args {
+  const uint8_t* rgb;  // [N][H][W][3]
+  float* out;          // [P][OH][OW][32]
+  const float* w;      // [2][26][32]
+  const float* bias;   // [2][32]
+  int P, nimg, H, W, OH, OW, pad_y, pad_x, tiles_x;
+};
+
+struct Dconv8Args {
+  const float* in;   // [P][H][W][64]
+  uint8_t* out_u8;   // [N][2H][2W][3]
+  float* out_f32;    // optional clipped fp32 RGB, same layout
+  const float* w;    // [2][25 phase-taps][64]
+  const float* bias; // [2]
+  int nimg, H, W, tiles_x;
+};
+
+hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
+hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);
+hipError_t launch_conv1(Conv1Args a, hipStream_t st);
+hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);
+hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st);
+hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
+
+}  // namespace nic

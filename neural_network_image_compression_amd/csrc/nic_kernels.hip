@@ -1,0 +1,654 @@
+// HIP kernels for the learned-image-codec hot path on gfx950 (MI355X / CDNA4).
+//
+// Reference path (AlexFuster/Neural_network_image_compression, tf2_0/src):
+//   Encoder.__call__ (encoder.py:38-47): u8 RGB -> /255 -> YCbCr (utils.py:64-77)
+//     -> BaseEncoder (encoder.py:19-32) per plane -> clip -> round(x*255) -> u8 latent (N,h,w,96)
+//   Decoder.__call__ (decoder.py:39-48): u8 latent -> /255 -> split -> BaseDecoder
+//     (decoder.py:19-32) per plane -> inverse YCbCr (utils.py:70-72) -> clip -> round -> u8 RGB
+//
+// Activations live in HBM as fp32 NHWC "plane batches": P = 3N planes ordered
+// [Y_0..Y_{N-1}, Cb_0..Cb_{N-1}, Cr_0..Cr_{N-1}] (the concat order of training.py:81-85 /
+// tf1_13/src/training.py:62).  Plane p uses model (p >= N) -- Y weights for p < N, the
+// shared CbCr weights otherwise (utils.py:19-24).  One launch covers all 3N planes.
+//
+// Convolutions with Cin >= 32 are implicit GEMMs on the exact-fp32 MFMA
+// v_mfma_f32_32x32x2_f32 (M = output pixels, N = Cout, K = taps x Cin): the input halo of a
+// block's output tile is staged once in LDS and re-read by every tap; weights are
+// pre-permuted on the host into MFMA fragment order and read from L2 as 16-B loads.
+// Conv2DTranspose (stride 2) is run as its 4-phase sub-pixel decomposition (taps 2x2, 2x3,
+// 3x2, 3x3) so no zero is ever multiplied.  Cin = 1 (conv1) and Cout = 1 (dconv8) layers
+// fuse the colour transforms and use MFMA over taps / VALU dot products respectively.
+//
+// Numerics: this file is compiled with -ffp-contract=off so every elementwise op rounds
+// like TF's one-op-at-a-time eager execution; products inside convolutions are exact-fp32
+// FMA chains (MFMA or explicit fmaf).  Quantisers use rintf (round half to even, = np.round).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nic_kernels.h"
+
+namespace nic {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__constant__ float c_u8_to_unit[256];  // fp32(i) / 255, correctly rounded (host-computed)
+__constant__ float c_ycbcr[9];         // fp32(ycbcr_kernel), utils.py:7
+__constant__ float c_ycbcr_inv[9];     // fp32(inv(ycbcr_kernel)), utils.py:8
+__constant__ float c_ycbcr_off[3];     // fp32(ycbcr_off), utils.py:9
+
+__device__ __forceinline__ float leaky02(float z) {
+  // tf.nn.leaky_relu(z, alpha=0.2) = max(alpha*z, z)
+  return fmaxf(__fmul_rn(z, 0.2f), z);
+}
+__device__ __forceinline__ float clip01(float v) {
+  // tf.clip_by_value(v, 0, 1) = max(min(v, 1), 0)
+  return fmaxf(fminf(v, 1.0f), 0.0f);
+}
+__device__ __forceinline__ uint8_t quant255(float v) {
+  // np.round(v * 255).astype(np.uint8) for v in [0, 1]: fp32 multiply, round half to even
+  return (uint8_t)(int)rintf(__fmul_rn(v, 255.0f));
+}
+// ((t0*k0 + t1*k1) + t2*k2), every op rounded (utils.py:64-68)
+__device__ __forceinline__ float project(const float* k, float t0, float t1, float t2) {
+  return __fadd_rn(__fadd_rn(__fmul_rn(t0, k[0]), __fmul_rn(t1, k[1])), __fmul_rn(t2, k[2]));
+}
+
+// ------------------------------------------------------------------------------------
+// Generic implicit-GEMM convolution on fp32 MFMA.
+//
+// Block = 4 waves (256 threads).  Output tile TH x TW pixels (forward conv) or TH x TW
+// coarse positions x 4 phases (stride-2 transposed conv).  Waves are arranged WM x WN x WK
+// over (M tiles, N tiles, taps); WK > 1 splits the taps and reduces through LDS.
+//
+// MFMA 32x32x2 f32 operand maps (cdna_hip_programming.md §3): lane l holds A[i=l&31][k=l>>5],
+// B[k=l>>5][j=l&31]; D register r of lane l is row (r&3)+8*(r>>2)+4*(l>>5), column l&31.
+// K ordering inside one tap: for ci-group q (8 channels) and r = 0..3 the k-pair of one MFMA
+// is (ci = 8q + r for lane half 0, ci = 8q + 4 + r for lane half 1).  A lane therefore reads
+// 4 consecutive channels of one pixel with a single ds_read_b128, and the host repacks the
+// weights as W[model][tap][q][h][co][r] so its B fragment is one 16-B global load.
+// ------------------------------------------------------------------------------------
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK>
+struct ConvGeom {
+  static_assert(WM * WN * WK == 4, "4 waves per block");
+  static_assert(CIN % 8 == 0 && COUT % 32 == 0, "channel tiling");
+  static_assert((TH * TW) % 32 == 0, "M tile is 32 pixels");
+  static constexpr int MT = TH * TW / 32;
+  static constexpr int NT = COUT / 32;
+  static_assert(MT % WM == 0 && NT % WN == 0, "wave split");
+  static constexpr int MTW = MT / WM;
+  static constexpr int NTW = NT / WN;
+  static constexpr int HH = TR ? TH + 2 : (TH - 1) * S + KS;
+  static constexpr int HW = TR ? TW + 2 : (TW - 1) * S + KS;
+  static constexpr int PS = CIN + 4;  // LDS pixel stride (floats), 16-B aligned, bank skew
+  static constexpr int NQ = CIN / 8;
+  static constexpr int NTAPS = KS * KS;
+  static constexpr int HALO_FLOATS = HH * HW * PS;
+  static constexpr int RED_FLOATS = (WK > 1) ? (WK - 1) * WM * WN * MTW * NTW * 16 * 64 : 0;
+  static constexpr int LDS_FLOATS = HALO_FLOATS > RED_FLOATS ? HALO_FLOATS : RED_FLOATS;
+};
+
+template <int IN_MODE, int CIN>
+__device__ __forceinline__ void stage_halo(float* lds, const ConvArgs& a, int p, int gy0, int gx0,
+                                           int HH, int HW, int PS) {
+  if constexpr (IN_MODE == IN_F32) {
+    const float* inp = a.in + (size_t)p * a.H * a.W * CIN;
+    constexpr int C4 = CIN / 4;
+    const int total = HH * HW * C4;
+    for (int idx = threadIdx.x; idx < total; idx += 256) {
+      const int pix = idx / C4, c4 = idx - pix * C4;
+      const int hy = pix / HW, hx = pix - hy * HW;
+      const int gy = gy0 + hy, gx = gx0 + hx;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+        v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * CIN + c4 * 4);
+      *(f32x4*)(lds + pix * PS + c4 * 4) = v;
+    }
+  } else {
+    // u8 latent (N, h, w, 96): plane p = (type, n), channels type*32 .. type*32+31,
+    // dequantised as x.astype(f32)/255 (decoder.py:40-41).
+    static_assert(CIN == 32, "latent planes carry 32 channels");
+    const int n = p % a.nimg, type = p / a.nimg;
+    const uint8_t* inp = a.in_u8 + (size_t)n * a.H * a.W * 96 + type * 32;
+    const int total = HH * HW * 8;  // 8 groups of 4 channels
+    for (int idx = threadIdx.x; idx < total; idx += 256) {
+      const int pix = idx >> 3, c4 = idx & 7;
+      const int hy = pix / HW, hx = pix - hy * HW;
+      const int gy = gy0 + hy, gx = gx0 + hx;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        const uint32_t q = *(const uint32_t*)(inp + ((size_t)gy * a.W + gx) * 96 + c4 * 4);
+        v[0] = c_u8_to_unit[q & 255];
+        v[1] = c_u8_to_unit[(q >> 8) & 255];
+        v[2] = c_u8_to_unit[(q >> 16) & 255];
+        v[3] = c_u8_to_unit[q >> 24];
+      }
+      *(f32x4*)(lds + pix * PS + c4 * 4) = v;
+    }
+  }
+}
+
+// Epilogue for one 32x32 accumulator tile: bias, leaky, optional residual add, optional
+// clip + quantise to the latent layout.  (oy_of, ox_of) map the tile row to output coords.
+template <int COUT, int OUT_MODE, bool RESID>
+__device__ __forceinline__ void store_tile(const ConvArgs& a, int p, int model, int nt, const f32x16& acc,
+                                           const int* oy_of, const int* ox_of) {
+  const int lane = threadIdx.x & 63;
+  const int co = nt * 32 + (lane & 31);
+  const float b = a.bias[model * COUT + co];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int oy = oy_of[r], ox = ox_of[r];
+    if (oy < a.OH && ox < a.OW) {
+      float v = leaky02(__fadd_rn(acc[r], b));  // Conv -> BiasAdd -> leaky_relu
+      const size_t o = (((size_t)p * a.OH + oy) * a.OW + ox) * COUT + co;
+      if constexpr (RESID) v = __fadd_rn(v, a.res[o]);  // x = x + res (encoder.py:25, decoder.py:29)
+      if constexpr (OUT_MODE == OUT_F32) {
+        a.out[o] = v;
+      } else {
+        // final layer: tf.clip_by_value(x, 0, 1) (encoder.py:32); concat planes on the
+        // channel axis (encoder.py:45); round(x*255) -> u8 (encoder.py:47)
+        v = clip01(v);
+        const int n = p % a.nimg, type = p / a.nimg;
+        const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co;
+        a.out_u8[lo] = quant255(v);
+        if (a.out_f32_latent) a.out_f32_latent[lo] = v;
+      }
+    }
+  }
+}
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
+          int OUT_MODE, bool RESID>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+  using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
+  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+
+  const int p = blockIdx.y;
+  const int tile = blockIdx.x;
+  const int tyi = tile / a.tiles_x;
+  const int t0y = tyi * TH, t0x = (tile - tyi * a.tiles_x) * TW;
+  const int model = p >= a.nimg ? 1 : 0;
+
+  int gy0, gx0;
+  if constexpr (TR) {
+    gy0 = t0y - 1;
+    gx0 = t0x - 1;
+  } else {
+    gy0 = t0y * S - a.pad_y;
+    gx0 = t0x * S - a.pad_x;
+  }
+  stage_halo<IN_MODE, CIN>(lds, a, p, gy0, gx0, G::HH, G::HW, G::PS);
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
+
+  // Per-lane A base offsets (floats) for each of this wave's M tiles.
+  int a_off[G::MTW];
+#pragma unroll
+  for (int i = 0; i < G::MTW; ++i) {
+    const int m = (wm * G::MTW + i) * 32 + (lane & 31);
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+    a_off[i] = TR ? (ty * G::HW + tx) * G::PS : (ty * S * G::HW + tx * S) * G::PS;
+    a_off[i] += half * 4;
+  }
+  const float* wbase = a.w + (size_t)model * G::NTAPS * CIN * COUT;
+  const int wlane = (half * COUT + (lane & 31)) * 4;
+
+  if constexpr (!TR) {
+    f32x16 acc[G::MTW][G::NTW];
+#pragma unroll
+    for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NTW; ++j) acc[i][j] = (f32x16){};
+
+    const int t_begin = wk * G::NTAPS / WK, t_end = (wk + 1) * G::NTAPS / WK;
+    for (int t = t_begin; t < t_end; ++t) {
+      const int kh = t / KS, kw = t - (t / KS) * KS;
+      const int toff = (kh * G::HW + kw) * G::PS;
+      const float* wt = wbase + (size_t)t * CIN * COUT + wlane;
+      f32x4 bq[G::NQ][G::NTW];
+#pragma unroll
+      for (int q = 0; q < G::NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j)
+          bq[q][j] = *(const f32x4*)(wt + q * 8 * COUT + (wn * G::NTW + j) * 128);
+#pragma unroll
+      for (int q = 0; q < G::NQ; ++q) {
+        f32x4 av[G::MTW];
+#pragma unroll
+        for (int i = 0; i < G::MTW; ++i) av[i] = *(const f32x4*)(lds + a_off[i] + toff + q * 8);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+            for (int j = 0; j < G::NTW; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][r], bq[q][j][r], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    if constexpr (WK > 1) {
+      // split-K: waves wk>0 park their partial sums in LDS (after every wave is done
+      // reading the halo), wave group 0 adds them in wk order and stores.
+      __syncthreads();
+      const int grp = wm + WM * wn;
+      if (wk > 0) {
+#pragma unroll
+        for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+          for (int j = 0; j < G::NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              lds[((((wk - 1) * WM * WN + grp) * G::MTW + i) * G::NTW + j) * 1024 + r * 64 + lane] = acc[i][j][r];
+      }
+      __syncthreads();
+      if (wk > 0) return;
+#pragma unroll
+      for (int k = 1; k < WK; ++k)
+#pragma unroll
+        for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+          for (int j = 0; j < G::NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              acc[i][j][r] = __fadd_rn(
+                  acc[i][j][r], lds[((((k - 1) * WM * WN + grp) * G::MTW + i) * G::NTW + j) * 1024 + r * 64 + lane]);
+    }
+
+#pragma unroll
+    for (int i = 0; i < G::MTW; ++i) {
+      int oy[16], ox[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * G::MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        oy[r] = t0y + m / TW;
+        ox[r] = t0x + m % TW;
+      }
+#pragma unroll
+      for (int j = 0; j < G::NTW; ++j)
+        store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * G::NTW + j, acc[i][j], oy, ox);
+    }
+  } else {
+    static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases");
+    // Phase (py, px) of output (2m+py, 2n+px) gathers input (m+dy, n+dx) for dy in
+    // {-1,0} (py=0) or {-1,0,1} (py=1), kernel tap t = py + 3 - 2*(dy+1).  Weights are
+    // stored phase-major in the same tap order.
+    int tap_base = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      const int ny = py ? 3 : 2, nx = px ? 3 : 2;
+      f32x16 acc[G::MTW][G::NTW];
+#pragma unroll
+      for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j) acc[i][j] = (f32x16){};
+      for (int iy = 0; iy < ny; ++iy) {
+        for (int ix = 0; ix < nx; ++ix) {
+          const int t = tap_base + iy * nx + ix;
+          // halo origin is (m0-1, n0-1): input (m+dy) sits at halo row m-m0+dy+1 = ty+iy
+          const int toff = (iy * G::HW + ix) * G::PS;
+          const float* wt = wbase + (size_t)t * CIN * COUT + wlane;
+          f32x4 bq[G::NQ][G::NTW];
+#pragma unroll
+          for (int q = 0; q < G::NQ; ++q)
+#pragma unroll
+            for (int j = 0; j < G::NTW; ++j)
+              bq[q][j] = *(const f32x4*)(wt + q * 8 * COUT + (wn * G::NTW + j) * 128);
+#pragma unroll
+          for (int q = 0; q < G::NQ; ++q) {
+            f32x4 av[G::MTW];
+#pragma unroll
+            for (int i = 0; i < G::MTW; ++i) av[i] = *(const f32x4*)(lds + a_off[i] + toff + q * 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+                for (int j = 0; j < G::NTW; ++j)
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][r], bq[q][j][r], acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::MTW; ++i) {
+        int oy[16], ox[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = (wm * G::MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          oy[r] = 2 * (t0y + m / TW) + py;
+          ox[r] = 2 * (t0x + m % TW) + px;
+        }
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j)
+          store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * G::NTW + j, acc[i][j], oy, ox);
+      }
+      tap_base += ny * nx;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
+// utils.py:74-77).  Block: 16x16 output pixels of one plane, 4 waves x 2 M tiles x 32 co.
+// K = 25 taps padded to 26 (13 MFMAs); lane half h supplies tap 2s+h of step s.
+// ------------------------------------------------------------------------------------
+constexpr int C1_T = 16;
+constexpr int C1_HH = (C1_T - 1) * 2 + 5;  // 35
+constexpr int C1_PS = C1_HH + 1;           // 36 (row stride)
+
+__global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
+  __shared__ float plane[C1_HH * C1_PS];
+  const int p = blockIdx.y;
+  const int n = p % a.nimg, type = p / a.nimg;
+  const int model = type > 0 ? 1 : 0;
+  const int tyi = blockIdx.x / a.tiles_x;
+  const int t0y = tyi * C1_T, t0x = (blockIdx.x - tyi * a.tiles_x) * C1_T;
+  const int gy0 = t0y * 2 - a.pad_y, gx0 = t0x * 2 - a.pad_x;
+  const uint8_t* img = a.rgb + (size_t)n * a.H * a.W * 3;
+  const float* k = c_ycbcr + type * 3;
+  const float off = c_ycbcr_off[type];
+  for (int idx = threadIdx.x; idx < C1_HH * C1_HH; idx += 256) {
+    const int hy = idx / C1_HH, hx = idx - hy * C1_HH;
+    const int gy = gy0 + hy, gx = gx0 + hx;
+    float v = 0.f;  // SAME zero padding of the colour plane
+    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+      const uint8_t* px = img + ((size_t)gy * a.W + gx) * 3;
+      const float r = c_u8_to_unit[px[0]], g = c_u8_to_unit[px[1]], b = c_u8_to_unit[px[2]];
+      v = __fadd_rn(project(k, r, g, b), off);
+    }
+    plane[hy * C1_PS + hx] = v;
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  // B fragments: W1[model][tap 0..25][co], tap 25 is zero padding
+  float bw[13];
+  const float* w = a.w + model * 26 * 32 + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < 13; ++s) bw[s] = w[(2 * s + half) * 32];
+  const float bias = a.bias[model * 32 + (lane & 31)];
+
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int mt = wave * 2 + i;
+    const int m = mt * 32 + (lane & 31);
+    const int ty = m / C1_T, tx = m % C1_T;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      int tap = 2 * s + half;
+      if (tap > 24) tap = 24;  // weight is zero; any finite operand
+      const int kh = tap / 5, kw = tap % 5;
+      const float av = plane[(ty * 2 + kh) * C1_PS + tx * 2 + kw];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mr = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const int oy = t0y + mr / C1_T, ox = t0x + mr % C1_T;
+      if (oy < a.OH && ox < a.OW)
+        a.out[(((size_t)p * a.OH + oy) * a.OW + ox) * 32 + (lane & 31)] = leaky02(__fadd_rn(acc[r], bias));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// dconv8 (64 -> 1, transposed k5 s2) fused with the inverse colour transform and output
+// quantiser (decoder.py:31-32, 45-48; utils.py:70-72).  One thread per coarse input
+// position computes its 4 output phases for the Y, Cb and Cr planes of one image, then
+// converts to RGB.  Cin is staged through LDS 16 channels at a time.
+// ------------------------------------------------------------------------------------
+constexpr int D8_T = 16;
+constexpr int D8_HH = D8_T + 2;  // 18
+constexpr int D8_CC = 16;        // channels per LDS chunk
+constexpr int D8_PS = D8_CC + 4; // pixel stride in LDS (floats)
+
+__global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
+  __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HH * D8_PS];
+  const int n = blockIdx.y;
+  const int tyi = blockIdx.x / a.tiles_x;
+  const int t0y = tyi * D8_T, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_T;
+  const int ty = threadIdx.x / D8_T, tx = threadIdx.x % D8_T;
+  float outv[3][4];
+
+  for (int type = 0; type < 3; ++type) {
+    const int p = type * a.nimg + n;
+    const int model = type > 0 ? 1 : 0;
+    const float* inp = a.in + (size_t)p * a.H * a.W * 64;
+    const float* w = a.w + model * 25 * 64;  // [phase-tap][ci]
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < 64; c0 += D8_CC) {
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < D8_HH * D8_HH * (D8_CC / 4); idx += 256) {
+        const int pix = idx / (D8_CC / 4), c4 = idx % (D8_CC / 4);
+        const int hy = pix / D8_HH, hx = pix % D8_HH;
+        const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+          v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * 64 + c0 + c4 * 4);
+        *(f32x4*)(halo + pix * D8_PS + c4 * 4) = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c4 = 0; c4 < D8_CC / 4; ++c4) {
+        f32x4 x[3][3];
+#pragma unroll
+        for (int iy = 0; iy < 3; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < 3; ++ix)
+            x[iy][ix] = *(const f32x4*)(halo + ((ty + iy) * D8_HH + tx + ix) * D8_PS + c4 * 4);
+        int tb = 0;
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          const int py = ph >> 1, px = ph & 1;
+          const int ny = py ? 3 : 2, nx = px ? 3 : 2;
+#pragma unroll
+          for (int iy = 0; iy < ny; ++iy)
+#pragma unroll
+            for (int ix = 0; ix < nx; ++ix) {
+              const float* wt = w + (tb + iy * nx + ix) * 64 + c0 + c4 * 4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[ph] = fmaf(x[iy][ix][r], wt[r], acc[ph]);
+            }
+          tb += ny * nx;
+        }
+      }
+    }
+    const float b = a.bias[model];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
+  }
+
+  const int my = t0y + ty, mx = t0x + tx;
+  if (my >= a.H || mx >= a.W) return;
+  const int OH = a.H * 2, OW = a.W * 2;
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    const int oy = 2 * my + (ph >> 1), ox = 2 * mx + (ph & 1);
+    // convert_to_rgb: (Y - 0, Cb - .5, Cr - .5) projected by fp32(inv kernel), then clip
+    const float t0 = __fsub_rn(outv[0][ph], c_ycbcr_off[0]);
+    const float t1 = __fsub_rn(outv[1][ph], c_ycbcr_off[1]);
+    const float t2 = __fsub_rn(outv[2][ph], c_ycbcr_off[2]);
+    const size_t o = (((size_t)n * OH + oy) * OW + ox) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = clip01(project(c_ycbcr_inv + 3 * c, t0, t1, t2));
+      a.out_u8[o + c] = quant255(v);
+      if (a.out_f32) a.out_f32[o + c] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Histogram entropy (tf1_13/src/training.py:66-71) and bitstream pack/unpack
+// (utils.py:35-40).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restrict__ z, int nimg, int plane_px,
+                                                          uint32_t* __restrict__ counts, int chunk_px) {
+  // grid: (chunks, 3N).  Block counts codes of plane p (= type*N + n) over pixels
+  // [chunk*chunk_px, ...) into an LDS histogram, then one atomic per non-empty bin.
+  __shared__ uint32_t h[256];
+  const int p = blockIdx.y;
+  const int n = p % nimg, type = p / nimg;
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint8_t* base = z + (size_t)n * plane_px * 96 + type * 32;
+  const int px0 = blockIdx.x * chunk_px;
+  const int px1 = min(px0 + chunk_px, plane_px);
+  // each pixel holds 32 contiguous codes = 2 x 16 B
+  for (int idx = px0 * 2 + threadIdx.x; idx < px1 * 2; idx += 256) {
+    const int px = idx >> 1, part = idx & 1;
+    const uint4 v = *(const uint4*)(base + (size_t)px * 96 + part * 16);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      atomicAdd(&h[w[k] & 255], 1u);
+      atomicAdd(&h[(w[k] >> 8) & 255], 1u);
+      atomicAdd(&h[(w[k] >> 16) & 255], 1u);
+      atomicAdd(&h[w[k] >> 24], 1u);
+    }
+  }
+  __syncthreads();
+  const uint32_t c = h[threadIdx.x];
+  if (c) atomicAdd(&counts[(size_t)p * 256 + threadIdx.x], c);
+}
+
+__global__ __launch_bounds__(256) void hist_entropy_kernel(const uint32_t* __restrict__ counts, float n_sym,
+                                                           float* __restrict__ bits) {
+  // one block per plane: p_i = c_i / N (fp32), term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2)
+  __shared__ double part[4];
+  const int p = blockIdx.x;
+  const float pr = __fdiv_rn((float)counts[(size_t)p * 256 + threadIdx.x], n_sym);
+  const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
+  const float term = __fmul_rn(pr, __fdiv_rn(-lg, 0.693147182464599609375f));
+  double s = (double)term;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bits[p] = (float)(((part[0] + part[1]) + part[2]) + part[3]);
+}
+
+__global__ __launch_bounds__(256) void pack_latent_kernel(const uint8_t* __restrict__ z, uint8_t* __restrict__ out,
+                                                          size_t plane_elems, int nimg) {
+  // packed[n][f / (8w)][f % (8w)][p] = z[n][(f/32) / w][(f/32) % w][32p + f % 32],
+  // i.e. flat index f of plane p in (n, 4h, 8w) equals flat index f of (n, h, w, 32).
+  const size_t total = (size_t)nimg * plane_elems;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t n = i / plane_elems, f = i - n * plane_elems;
+    const size_t src = n * plane_elems * 3 + (f >> 5) * 96 + (f & 31);
+    uint8_t* dst = out + (n * plane_elems + f) * 3;
+    dst[0] = z[src];
+    dst[1] = z[src + 32];
+    dst[2] = z[src + 64];
+  }
+}
+
+__global__ __launch_bounds__(256) void unpack_latent_kernel(const uint8_t* __restrict__ img, uint8_t* __restrict__ z,
+                                                            size_t plane_elems, int nimg) {
+  const size_t total = (size_t)nimg * plane_elems;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t n = i / plane_elems, f = i - n * plane_elems;
+    const size_t dst = n * plane_elems * 3 + (f >> 5) * 96 + (f & 31);
+    const uint8_t* src = img + (n * plane_elems + f) * 3;
+    z[dst] = src[0];
+    z[dst + 32] = src[1];
+    z[dst + 64] = src[2];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
+          int OUT_MODE, bool RESID>
+static hipError_t launch_conv(ConvArgs a, hipStream_t st) {
+  const int gy = TR ? a.H : a.OH, gx = TR ? a.W : a.OW;  // tile grid over coarse / output coords
+  const int tiles_y = (gy + TH - 1) / TH;
+  a.tiles_x = (gx + TW - 1) / TW;
+  dim3 grid(tiles_y * a.tiles_x, a.P);
+  hipLaunchKernelGGL((conv_mfma_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>), grid,
+                     dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off) {
+  hipError_t e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_u8_to_unit), u8_to_unit, 256 * sizeof(float))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_ycbcr), ycbcr, 9 * sizeof(float))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_ycbcr_inv), ycbcr_inv, 9 * sizeof(float))) != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_ycbcr_off), off, 3 * sizeof(float));
+}
+
+hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st) {
+  switch (id) {
+    // encoder (conv1 has its own kernel)
+    case L_CONV2:  // 32->64 k5 s2: 8x8 tile, 4 waves = 2(M) x 2(N)
+      return launch_conv<32, 64, 5, 2, false, 8, 8, 2, 2, 1, IN_F32, OUT_F32, false>(a, st);
+    case L_CONV3:  // 64->64 k3 s1: 8x16 tile, 4 waves along M, each 32 px x 64 co
+      return launch_conv<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, st);
+    case L_CONV4:  // + residual
+      return launch_conv<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, st);
+    case L_CONV8:  // 64->32 k5 s2 -> u8 latent: 4x8 tile, taps split over the 4 waves
+      return launch_conv<64, 32, 5, 2, false, 4, 8, 1, 1, 4, IN_F32, OUT_U8_LATENT, false>(a, st);
+    // decoder (dconv8 has its own kernel)
+    case L_DCONV1:  // latent u8 -> 64, transposed k5 s2: 8x8 coarse tile, 2(M) x 2(N)
+      return launch_conv<32, 64, 5, 2, true, 8, 8, 2, 2, 1, IN_U8_LATENT, OUT_F32, false>(a, st);
+    case L_DCONV5:  // transposed k3 s1 == conv k3 s1 with flipped kernel
+      return launch_conv<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, st);
+    case L_DCONV6:
+      return launch_conv<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, st);
+    case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tile, 4 waves along M
+      return launch_conv<64, 64, 5, 2, true, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_conv1(Conv1Args a, hipStream_t st) {
+  const int tiles_y = (a.OH + C1_T - 1) / C1_T;
+  a.tiles_x = (a.OW + C1_T - 1) / C1_T;
+  hipLaunchKernelGGL(conv1_colour_kernel, dim3(tiles_y * a.tiles_x, a.P), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
+  const int tiles_y = (a.H + D8_T - 1) / D8_T;
+  a.tiles_x = (a.W + D8_T - 1) / D8_T;
+  hipLaunchKernelGGL(dconv8_colour_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(counts, 0, (size_t)3 * nimg * 256 * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  const int chunk_px = 1024;
+  const int chunks = (plane_px + chunk_px - 1) / chunk_px;
+  hipLaunchKernelGGL(latent_hist_kernel, dim3(chunks, 3 * nimg), dim3(256), 0, st, z, nimg, plane_px, counts,
+                     chunk_px);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (bits) {
+    hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(256), 0, st, counts, (float)plane_px * 32.0f, bits);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+hipError_t launch_pack(const uint8_t* z, uint8_t* out, int nimg, int h8, int w8, bool unpack, hipStream_t st) {
+  const size_t plane_elems = (size_t)h8 * w8 * 32;
+  const size_t total = plane_elems * nimg;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  if (unpack)
+    hipLaunchKernelGGL(unpack_latent_kernel, dim3(blocks), dim3(256), 0, st, z, out, plane_elems, nimg);
+  else
+    hipLaunchKernelGGL(pack_latent_kernel, dim3(blocks), dim3(256), 0, st, z, out, plane_elems, nimg);
+  return hipGetLastError();
+}
+
+}  // namespace nic

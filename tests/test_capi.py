@@ -1,0 +1,75 @@
+"""CPU-side checks of the C-ABI library: it is built, loads, exports exactly what
+include/nic.h declares, and its host-only entry points behave (no GPU calls here)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from neural_network_image_compression_amd import _lib
+from oracle import nic_oracle as O
+
+
+def test_library_built_and_loads():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build()"
+    L = _lib.lib()
+    assert L.nic_version() >= 100
+
+
+def test_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(L, s), f"libnic.so does not export {s}"
+    assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with nic.h"
+
+
+def test_exports_are_c_linkage():
+    out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
+    for s in _lib.header_symbols():
+        assert f" T {s}\n" in out
+
+
+@pytest.mark.parametrize("h,w", [(256, 256), (2160, 3840), (37, 53), (1, 1), (8, 9), (512, 768)])
+def test_latent_shape_matches_tf_same(h, w):
+    hh, ww = h, w
+    for _ in range(3):
+        hh, ww = O.same_pads(hh, 5, 2)[0], O.same_pads(ww, 5, 2)[0]
+    assert _lib.latent_shape(h, w) == (hh, ww)
+
+
+def test_latent_shape_rejects_bad_sizes():
+    with pytest.raises(ValueError):
+        _lib.latent_shape(0, 5)
+
+
+def test_device_constants_match_oracle():
+    k, kinv, off = _lib.constants()
+    np.testing.assert_array_equal(k, O.YCBCR_KERNEL)
+    np.testing.assert_array_equal(kinv, O.YCBCR_INV_KERNEL)
+    np.testing.assert_array_equal(off, O.YCBCR_OFF)
+
+
+def test_null_arguments_are_rejected_without_crashing():
+    L = _lib.lib()
+    assert L.nic_create(0, None) == _lib.NIC_EINVAL
+    assert L.nic_encode(None, None, 1, 8, 8, None, None, None) == _lib.NIC_EINVAL
+    assert "NULL" in _lib.last_error()
+    assert L.nic_decode(None, None, 1, 1, 1, None, None, None) == _lib.NIC_EINVAL
+    assert L.nic_set_weights(None, 0, b"conv1/kernel", None, None, 0) == _lib.NIC_EINVAL
+    assert L.nic_pack_latent(None, 1, 1, 1, None, None) == _lib.NIC_EINVAL
+    assert L.nic_pack_latent(None, 1, 0, 1, None, None) == _lib.NIC_ESHAPE
+    assert L.nic_pack_latent(None, 0, 1, 1, None, None) == _lib.NIC_OK  # empty batch
+    assert L.nic_set_timing(None, 1) == _lib.NIC_EINVAL
+    assert L.nic_destroy(None) == _lib.NIC_OK
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = _lib.lib().nic_create(0, ctypes.byref(h))
+    assert rc < 0 and not h.value
+    assert _lib.last_error()

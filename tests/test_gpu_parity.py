@@ -1,0 +1,247 @@
+"""GPU parity of the HIP path (through the C-ABI) against the CPU oracle.
+
+Parity contract, stated per test:
+  * integer stages (quantise, pack/unpack, histogram counts): bit-exact;
+  * encoder fp32 pre-quant latent: max |delta| <= 2e-5 vs the oracle;
+  * u8 codes: identical except where the oracle's x*255 lies within 1e-3 of a .5
+    rounding boundary (then +-1), and at most 0.1 % of codes;
+  * decoder fed the oracle's codes: u8 |delta| <= 1 and PSNR(build, oracle) >= 50 dB;
+  * end to end: |PSNR(x, x_hat_build) - PSNR(x, x_hat_oracle)| <= 0.1 dB;
+  * entropy: counts bit-exact, bits/symbol within 2e-6.
+Parity against TensorFlow itself is unpinned (no TF, no reference fixtures): the oracle
+stands in for it, see oracle/nic_oracle.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import nic_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+PREQUANT_ATOL = 2e-5
+BOUNDARY = 1e-3
+MAX_FLIP_FRAC = 1e-3
+RECON_PSNR_MIN = 50.0
+E2E_PSNR_TOL = 0.1
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.fixture(scope="module")
+def codecs(weights_spread, weights_glorot):
+    from neural_network_image_compression_amd.codec import Codec
+    a = Codec(0)
+    a.set_weights(weights_spread)
+    b = Codec(0)
+    b.set_weights(weights_glorot)
+    assert a.ready() == (True, True)
+    return {"spread": a, "glorot": b}
+
+
+def check_codes(z_gpu, z_ref, f_ref):
+    """u8 codes equal except within BOUNDARY of a .5 boundary of the oracle's x*255."""
+    diff = z_gpu.astype(np.int32) - z_ref.astype(np.int32)
+    bad = diff != 0
+    assert np.abs(diff).max(initial=0) <= 1
+    v = f_ref.astype(np.float64) * 255.0
+    near = np.abs(v - np.floor(v) - 0.5) < BOUNDARY
+    assert not np.any(bad & ~near), f"{np.count_nonzero(bad & ~near)} codes differ away from a rounding boundary"
+    assert np.count_nonzero(bad) <= MAX_FLIP_FRAC * bad.size
+    return int(np.count_nonzero(bad))
+
+
+def check_recon(r_gpu, r_ref):
+    d = np.abs(r_gpu.astype(np.int32) - r_ref.astype(np.int32))
+    assert d.max(initial=0) <= 1
+    assert O.psnr(r_gpu, r_ref) >= RECON_PSNR_MIN
+
+
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot"])
+def test_encode_matches_golden(case, codecs, golden, manifest):
+    g = golden(case)
+    c = codecs[manifest["cases"][case]["init"]]
+    z, f = c.encode(_dev(g["x"]), prequant=True)
+    z, f = z.cpu().numpy(), f.cpu().numpy()
+    assert z.shape == g["latent"].shape
+    assert np.abs(f - g["prequant"]).max() <= PREQUANT_ATOL
+    check_codes(z, g["latent"], g["prequant"])
+    # the fp32 latent the codes came from quantises exactly (integer stage bit-exact)
+    np.testing.assert_array_equal(O.quantise_u8(f), z)
+
+
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot"])
+def test_decode_matches_golden(case, codecs, golden, manifest):
+    g = golden(case)
+    c = codecs[manifest["cases"][case]["init"]]
+    r, rf = c.decode(_dev(g["latent"]), rgb_f32=True)
+    r, rf = r.cpu().numpy(), rf.cpu().numpy()
+    assert r.shape == g["recon"].shape
+    check_recon(r, g["recon"])
+    np.testing.assert_array_equal(O.quantise_u8(rf), r)
+
+
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4"])
+def test_end_to_end_psnr(case, codecs, golden, weights_spread):
+    g = golden(case)
+    c = codecs["spread"]
+    x = g["x"]
+    r = c.decode(c.encode(_dev(x))).cpu().numpy()
+    assert abs(O.psnr(x, r) - O.psnr(x, g["recon"])) <= E2E_PSNR_TOL
+
+
+@pytest.mark.parametrize("shape,seed", [((2, 24, 40), 1), ((1, 9, 17), 2), ((3, 8, 8), 3), ((1, 50, 31), 4),
+                                        ((1, 1, 1), 5), ((2, 72, 16), 6)])
+def test_random_shapes_vs_live_oracle(shape, seed, codecs, weights_spread):
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
+    c = codecs["spread"]
+    f_ref = O.encode_f32(weights_spread, x)
+    z_ref = O.quantise_u8(f_ref)
+    z, f = c.encode(_dev(x), prequant=True)
+    assert np.abs(f.cpu().numpy() - f_ref).max() <= PREQUANT_ATOL
+    check_codes(z.cpu().numpy(), z_ref, f_ref)
+    r = c.decode(_dev(z_ref)).cpu().numpy()
+    check_recon(r, O.decode(weights_spread, z_ref))
+
+
+def test_random_latents_decode(codecs, weights_spread):
+    """Decoder on codes spanning the full u8 range (not just encoder outputs)."""
+    rng = np.random.default_rng(11)
+    z = rng.integers(0, 256, (2, 5, 6, 96), dtype=np.uint8)
+    r = codecs["spread"].decode(_dev(z)).cpu().numpy()
+    check_recon(r, O.decode(weights_spread, z))
+
+
+def test_batch_invariance_and_determinism(codecs, golden):
+    """Each image's result is bit-identical alone or inside a batch, and run to run."""
+    x = golden("imagenet4")["x"]
+    c = codecs["spread"]
+    zb, fb = c.encode(_dev(x), prequant=True)
+    zb2 = c.encode(_dev(x))
+    assert torch.equal(zb, zb2)
+    rb = c.decode(zb)
+    for i in range(x.shape[0]):
+        zi, fi = c.encode(_dev(x[i:i + 1]), prequant=True)
+        assert torch.equal(zi[0], zb[i]) and torch.equal(fi[0], fb[i])
+        assert torch.equal(c.decode(zi)[0], rb[i])
+
+
+def test_full_size_batch_properties(codecs, weights_spread):
+    """BASELINE config 2 size (64 x 256^2): deterministic, and two sampled images agree with
+    the oracle at full size."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 256, (64, 256, 256, 3), generator=g, dtype=torch.uint8)
+    c = codecs["spread"]
+    xd = x.cuda()
+    z1 = c.encode(xd)
+    r1 = c.decode(z1)
+    z2 = c.encode(xd)
+    r2 = c.decode(z2)
+    assert torch.equal(z1, z2) and torch.equal(r1, r2)
+    for i in (0, 63):
+        xi = x[i:i + 1].numpy()
+        f_ref = O.encode_f32(weights_spread, xi)
+        check_codes(z1[i:i + 1].cpu().numpy(), O.quantise_u8(f_ref), f_ref)
+        check_recon(c.decode(_dev(O.quantise_u8(f_ref))).cpu().numpy(),
+                    O.decode(weights_spread, O.quantise_u8(f_ref)))
+
+
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "kodim21_glorot"])
+def test_entropy_matches_golden(case, codecs, golden):
+    g = golden(case)
+    bits, cnt = codecs["spread"].entropy(_dev(g["latent"]), counts=True)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), g["counts"])
+    np.testing.assert_allclose(bits.cpu().numpy(), g["bits"].ravel(), rtol=0, atol=2e-6)
+
+
+def test_entropy_large_and_edge_planes(codecs):
+    rng = np.random.default_rng(5)
+    z = rng.integers(0, 256, (1, 270, 480, 96), dtype=np.uint8)  # one 4K frame's latent
+    z[..., 32:64] = 7  # a constant plane: H = 0
+    bits, cnt = codecs["spread"].entropy(_dev(z), counts=True)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), O.histograms(z))
+    np.testing.assert_allclose(bits.cpu().numpy(), O.hist_entropy(z).ravel(), rtol=0, atol=2e-6)
+    assert bits[1].item() == 0.0
+
+
+def test_pack_unpack_bit_exact(codecs):
+    rng = np.random.default_rng(9)
+    z = rng.integers(0, 256, (3, 7, 5, 96), dtype=np.uint8)
+    c = codecs["spread"]
+    p = c.pack(_dev(z))
+    np.testing.assert_array_equal(p.cpu().numpy(), O.pack_latent(z))
+    np.testing.assert_array_equal(c.unpack(p).cpu().numpy(), z)
+
+
+def test_numpy_surface_matches_device(codecs, golden, weights_spread):
+    from neural_network_image_compression_amd.codec import Decoder, Encoder
+    g = golden("imagenet4")
+    enc = Encoder(codec=codecs["spread"])
+    dec = Decoder(codec=codecs["spread"])
+    z = enc(g["x"])
+    assert isinstance(z, np.ndarray) and z.dtype == np.uint8 and z.shape == g["latent"].shape
+    assert np.array_equal(z, codecs["spread"].encode(_dev(g["x"])).cpu().numpy())
+    r = dec(z)
+    assert r.shape == (4, 128, 128, 3)
+    with pytest.raises(ValueError):
+        enc(g["x"][0])  # 3-D input
+    with pytest.raises(ValueError):
+        enc(g["x"].astype(np.float32) + 0.5)  # not representable as u8 codes
+
+
+def test_errors_and_empty_batch(weights_spread):
+    from neural_network_image_compression_amd import _lib
+    from neural_network_image_compression_amd.codec import Codec
+    c = Codec(0)
+    with pytest.raises(_lib.NicError):
+        c.encode(torch.zeros((1, 8, 8, 3), dtype=torch.uint8, device="cuda"))  # no weights yet
+    with pytest.raises(ValueError):
+        c.set_tensor("encoderY", "conv1", "kernel", np.zeros((3, 3, 1, 32), np.float32))
+    with pytest.raises(ValueError):
+        c.set_tensor("encoderY", "conv9", "kernel", np.zeros((5, 5, 1, 32), np.float32))
+    c.set_weights(weights_spread)
+    z = c.encode(torch.zeros((0, 16, 16, 3), dtype=torch.uint8, device="cuda"))
+    assert z.shape == (0, 2, 2, 96)
+    with pytest.raises(TypeError):
+        c.encode(torch.zeros((1, 8, 8, 3), dtype=torch.float32, device="cuda"))
+
+
+def test_layer_timing(codecs):
+    c = codecs["spread"]
+    x = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, device="cuda")
+    c.set_timing(True)
+    for _ in range(3):
+        c.decode(c.encode(x))
+    t = c.layer_times()
+    c.set_timing(False)
+    assert all(n == 3 and ms > 0 for ms, n in t.values())
+
+
+def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden):
+    """Encoder.compress / Decoder.uncompress (encoder.py:49-51, decoder.py:50-52, utils.py:30-62)."""
+    from PIL import Image
+
+    from neural_network_image_compression_amd import weights as W
+    from neural_network_image_compression_amd.codec import Decoder, Encoder
+    ds = tmp_path / "kodak"
+    ds.mkdir()
+    g = golden("imagenet4")
+    for i in range(3):
+        Image.fromarray(g["x"][i]).save(ds / f"img{i}.png")
+    ck = str(tmp_path / "ckpt" / "encoder")
+    W.save(weights_spread, ck, "encoder")
+    W.save(weights_spread, str(tmp_path / "ckpt" / "decoder"), "decoder")
+    enc = Encoder(0)
+    enc.compress(str(ds), ck)
+    packed = np.array(Image.open(tmp_path / "kodak_compressed" / "img1.png"))
+    assert packed.shape == (64, 128, 3)
+    z = codecs["spread"].encode(_dev(g["x"][1:2])).cpu().numpy()
+    np.testing.assert_array_equal(packed, O.pack_latent(z)[0])
+    dec = Decoder(0)
+    dec.uncompress(str(tmp_path / "kodak_compressed"), str(tmp_path / "ckpt" / "decoder"))
+    rec = np.array(Image.open(tmp_path / "kodak_uncompressed" / "img1.png"))
+    np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
