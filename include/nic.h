@@ -58,6 +58,16 @@ enum {
   NIC_MODEL_DECODER_CBCR = 3
 };
 
+/* Arithmetic of the Cin >= 32 convolutions (conv2..conv8, dconv1..dconv7):
+ *   NIC_PRECISION_FP32  -- exact-fp32 MFMA (v_mfma_f32_32x32x2_f32): an fp32 FMA chain;
+ *   NIC_PRECISION_F16X3 -- split-f16 MFMA (default): each fp32 operand x = hi + lo with
+ *     hi, lo f16 and weights pre-scaled by 2^k; a*w ~ a_hi*w_hi + a_hi*w_lo + a_lo*w_hi on
+ *     v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Error ~2^-22 relative per product,
+ *     i.e. at the level of fp32 accumulation-order differences; ~5x the fp32 MFMA rate.
+ *     Requires |activations| < 65504 (f16 range).
+ * conv1, dconv8, colour transforms and quantisers are fp32 in both modes. */
+enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
+
 /* ABI version: major * 10000 + minor * 100 + patch */
 int nic_version(void);
 
@@ -80,6 +90,9 @@ int nic_destroy(nic_ctx* ctx);
  * The kernel is repacked to the device-native fragment layout.  Synchronous. */
 int nic_set_weights(nic_ctx* ctx, int model_id, const char* layer, const float* host, const int64_t* shape,
                     int ndim);
+
+int nic_set_precision(nic_ctx* ctx, int mode);
+int nic_get_precision(nic_ctx* ctx, int* mode);
 
 /* 1 when every tensor of the encoder pair (resp. decoder pair) has been set. */
 int nic_weights_ready(nic_ctx* ctx, int* encoder_ready, int* decoder_ready);

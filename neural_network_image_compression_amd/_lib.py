@@ -19,6 +19,10 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "nic.h")
 
 LAYER_NAMES = ("conv1", "conv2", "conv3", "conv4", "conv8", "dconv1", "dconv5", "dconv6", "dconv7", "dconv8")
 
+PRECISION_FP32 = 0
+PRECISION_F16X3 = 1
+PRECISIONS = {"fp32": PRECISION_FP32, "f16x3": PRECISION_F16X3}
+
 NIC_OK = 0
 NIC_EINVAL = -1
 NIC_ESHAPE = -2
@@ -48,6 +52,8 @@ _SIGNATURES = {
     "nic_encode": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_decode": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_entropy_hist": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "nic_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "nic_get_precision": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),
     "nic_set_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_layer_times": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "nic_pack_latent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),

@@ -51,7 +51,7 @@ def _as_u8_array(x, what: str) -> np.ndarray:
 class Codec:
     """One ``nic_ctx`` on one HIP device: weights + workspace for encode/decode/entropy."""
 
-    def __init__(self, device: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, precision: str = "f16x3"):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("neural_network_image_compression_amd needs a ROCm GPU (no CPU fallback)")
@@ -61,6 +61,7 @@ class Codec:
         _lib.check(self._L.nic_create(self.device, ctypes.byref(h)), "nic_create")
         self._h = h
         self._keep: Dict[str, np.ndarray] = {}
+        self.precision = precision
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -92,6 +93,19 @@ class Codec:
         e, d = ctypes.c_int(), ctypes.c_int()
         _lib.check(self._L.nic_weights_ready(self._h, ctypes.byref(e), ctypes.byref(d)), "nic_weights_ready")
         return bool(e.value), bool(d.value)
+
+    @property
+    def precision(self) -> str:
+        m = ctypes.c_int()
+        _lib.check(self._L.nic_get_precision(self._h, ctypes.byref(m)), "nic_get_precision")
+        return {v: k for k, v in _lib.PRECISIONS.items()}[m.value]
+
+    @precision.setter
+    def precision(self, mode: str) -> None:
+        """'f16x3' (default: split-f16 MFMA) or 'fp32' (exact fp32 MFMA) for the Cin>=32 convs."""
+        if mode not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, got {mode!r}")
+        _lib.check(self._L.nic_set_precision(self._h, _lib.PRECISIONS[mode]), "nic_set_precision")
 
     def set_timing(self, enable: bool) -> None:
         """Bracket every layer launch with hipEvents on the launch stream (resets the sums)."""

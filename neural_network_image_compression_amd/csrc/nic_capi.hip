@@ -86,6 +86,38 @@ void repack_fragments(std::vector<float>& out, int taps, int cin, int cout, F ge
           }
 }
 
+// Split-f16 fragment order: Wx[tap][s][hl][h][co][j] with ci = 16s + 8h + j, holding
+// hi = f16(w*2^k) (hl = 0) and lo = f16(w*2^k - hi) (hl = 1).  2^k is chosen per model so
+// that max|w*2^k| < 2^15: hi and lo stay normal f16 numbers.  Returns k.
+template <class F>
+int repack_x3(std::vector<uint16_t>& out, int taps, int cin, int cout, F get) {
+  float maxabs = 0.f;
+  for (int t = 0; t < taps; ++t)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int co = 0; co < cout; ++co) maxabs = std::max(maxabs, std::fabs(get(t, ci, co)));
+  int k = 0;
+  if (maxabs > 0.f && std::isfinite(maxabs)) {
+    int e = 0;
+    std::frexp(maxabs, &e);  // maxabs = m * 2^e, m in [0.5, 1)
+    k = std::min(std::max(15 - e, -100), 100);
+  }
+  out.assign((size_t)taps * cin * cout * 2, 0);
+  for (int t = 0; t < taps; ++t)
+    for (int s = 0; s < cin / 16; ++s)
+      for (int h = 0; h < 2; ++h)
+        for (int co = 0; co < cout; ++co)
+          for (int j = 0; j < 8; ++j) {
+            const int ci = 16 * s + 8 * h + j;
+            const float w = std::ldexp(get(t, ci, co), k);
+            const _Float16 hi = (_Float16)w;
+            const _Float16 lo = (_Float16)(w - (float)hi);
+            const size_t base = ((((size_t)t * (cin / 16) + s) * 2) * 2 + h) * cout * 8;
+            std::memcpy(&out[base + (size_t)co * 8 + j], &hi, 2);
+            std::memcpy(&out[base + (size_t)2 * cout * 8 + (size_t)co * 8 + j], &lo, 2);
+          }
+  return k;
+}
+
 // Phase-major tap enumeration of a k5 s2 Conv2DTranspose: for phase (py, px) and
 // halo offsets (iy, ix), the kernel tap is (py + 3 - 2*iy, px + 3 - 2*ix).
 template <class F>
@@ -98,36 +130,47 @@ void for_each_phase_tap(F f) {
   }
 }
 
-void repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out) {
+// Repack a Keras-layout kernel for the fp32 path (out) and, for the MFMA layers with
+// Cin >= 32, the split-f16 path (outx, returns the scale exponent k; -1000 if none).
+int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, std::vector<uint16_t>& outx) {
   const int k = L.k, cin = L.cin, cout = L.cout;
+  outx.clear();
   if (L.id == L_CONV1) {  // HWIO (5,5,1,32) -> [26][32], tap 25 = 0
     out.assign(26 * 32, 0.f);
     for (int t = 0; t < 25; ++t)
       for (int co = 0; co < 32; ++co) out[t * 32 + co] = K[t * 32 + co];
-  } else if (L.id == L_DCONV8) {  // (5,5,1,64) (kh,kw,Cout,Cin) -> [25 phase taps][64]
+    return -1000;
+  }
+  if (L.id == L_DCONV8) {  // (5,5,1,64) (kh,kw,Cout,Cin) -> [25 phase taps][64]
     out.assign(25 * 64, 0.f);
     for_each_phase_tap([&](int t, int ky, int kx) {
       for (int ci = 0; ci < 64; ++ci) out[t * 64 + ci] = K[((size_t)(ky * 5 + kx) * 1 + 0) * 64 + ci];
     });
-  } else if (!L.transposed) {  // HWIO
-    repack_fragments(out, k * k, cin, cout,
-                     [&](int t, int ci, int co) { return K[((size_t)t * cin + ci) * cout + co]; });
-  } else if (L.s == 1) {  // transposed k3 s1 == conv with flipped taps, swapped channels
-    repack_fragments(out, k * k, cin, cout, [&](int t, int ci, int co) {
+    return -1000;
+  }
+  if (!L.transposed) {  // HWIO
+    auto get = [&](int t, int ci, int co) { return K[((size_t)t * cin + ci) * cout + co]; };
+    repack_fragments(out, k * k, cin, cout, get);
+    return repack_x3(outx, k * k, cin, cout, get);
+  }
+  if (L.s == 1) {  // transposed k3 s1 == conv with flipped taps, swapped channels
+    auto get = [&](int t, int ci, int co) {
       const int u = t / k, v = t % k;
       const int ky = k - 1 - u, kx = k - 1 - v;
       return K[(((size_t)ky * k + kx) * cout + co) * cin + ci];
-    });
-  } else {  // transposed k5 s2, phase-major taps
-    std::vector<int> tap_ky(25), tap_kx(25);
-    for_each_phase_tap([&](int t, int ky, int kx) {
-      tap_ky[t] = ky;
-      tap_kx[t] = kx;
-    });
-    repack_fragments(out, 25, cin, cout, [&](int t, int ci, int co) {
-      return K[(((size_t)tap_ky[t] * 5 + tap_kx[t]) * cout + co) * cin + ci];
-    });
+    };
+    repack_fragments(out, k * k, cin, cout, get);
+    return repack_x3(outx, k * k, cin, cout, get);
   }
+  // transposed k5 s2, phase-major taps
+  std::vector<int> tap_ky(25), tap_kx(25);
+  for_each_phase_tap([&](int t, int ky, int kx) {
+    tap_ky[t] = ky;
+    tap_kx[t] = kx;
+  });
+  auto get = [&](int t, int ci, int co) { return K[(((size_t)tap_ky[t] * 5 + tap_kx[t]) * cout + co) * cin + ci]; };
+  repack_fragments(out, 25, cin, cout, get);
+  return repack_x3(outx, 25, cin, cout, get);
 }
 
 struct SamePad {
@@ -157,6 +200,9 @@ struct nic_ctx {
   int device = 0;
   float* wk[L_COUNT] = {};  // [2 models][packed kernel]
   float* wb[L_COUNT] = {};  // [2 models][cout]
+  uint16_t* wx[L_COUNT] = {};  // split-f16 kernels [2 models][taps*cin*cout*2]
+  float wscale[L_COUNT][2] = {};  // 2^-k per model for the split-f16 kernels
+  int precision = NIC_PRECISION_F16X3;
   bool have_k[4][5] = {};
   bool have_b[4][5] = {};
   char* ws = nullptr;
@@ -274,6 +320,10 @@ struct LayerTimer {
     if (_rc) return _rc;                           \
   } while (0)
 
+hipError_t run_layer(const nic_ctx* c, LayerId id, const ConvArgs& a, hipStream_t st) {
+  return c->precision == NIC_PRECISION_F16X3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st);
+}
+
 bool models_ready(const nic_ctx* c, int m0) {
   for (int m = m0; m < m0 + 2; ++m)
     for (int i = 0; i < 5; ++i)
@@ -325,12 +375,15 @@ int nic_create(int device, nic_ctx** out) {
     for (int i = 0; i < 5; ++i) {
       const LayerSpec& L = tab[i];
       const size_t kb = 2 * packed_kernel_floats(L) * sizeof(float), bb = 2 * L.cout * sizeof(float);
-      if (hipMalloc(&c->wk[L.id], kb) != hipSuccess || hipMalloc(&c->wb[L.id], bb) != hipSuccess) {
+      if (hipMalloc(&c->wk[L.id], kb) != hipSuccess || hipMalloc(&c->wb[L.id], bb) != hipSuccess ||
+          (L.cin >= 32 && L.cout >= 32 && hipMalloc(&c->wx[L.id], kb) != hipSuccess)) {
         nic_destroy(c);
         return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
       }
       (void)hipMemset(c->wk[L.id], 0, kb);
       (void)hipMemset(c->wb[L.id], 0, bb);
+      if (c->wx[L.id]) (void)hipMemset(c->wx[L.id], 0, kb);
+      c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
     }
   }
   // constants: u8 -> fp32 /255 (correctly rounded on the host), colour matrices
@@ -355,6 +408,7 @@ int nic_destroy(nic_ctx* c) {
   for (int i = 0; i < L_COUNT; ++i) {
     if (c->wk[i]) (void)hipFree(c->wk[i]);
     if (c->wb[i]) (void)hipFree(c->wb[i]);
+    if (c->wx[i]) (void)hipFree(c->wx[i]);
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
@@ -383,9 +437,15 @@ int nic_set_weights(nic_ctx* c, int model_id, const char* layer, const float* ho
       return fail(NIC_ESHAPE, "nic_set_weights: %s/kernel expects shape (%lld,%lld,%lld,%lld)", lname.c_str(),
                   (long long)want[0], (long long)want[1], (long long)want[2], (long long)want[3]);
     std::vector<float> packed;
-    repack_kernel(*L, host, packed);
+    std::vector<uint16_t> packedx;
+    const int kexp = repack_kernel(*L, host, packed, packedx);
     HIP_TRY(hipMemcpy(c->wk[L->id] + m * packed.size(), packed.data(), packed.size() * sizeof(float),
                       hipMemcpyHostToDevice));
+    if (!packedx.empty()) {
+      HIP_TRY(hipMemcpy(c->wx[L->id] + m * packedx.size(), packedx.data(), packedx.size() * sizeof(uint16_t),
+                        hipMemcpyHostToDevice));
+      c->wscale[L->id][m] = std::ldexp(1.0f, -kexp);
+    }
     c->have_k[model_id][idx] = true;
   } else if (kind == "bias") {
     if (ndim != 1 || shape[0] != L->cout)
@@ -472,6 +532,9 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
     a.out = out;
     a.res = res;
     a.w = c->wk[id];
+    a.wx = c->wx[id];
+    a.wscale[0] = c->wscale[id][0];
+    a.wscale[1] = c->wscale[id][1];
     a.bias = c->wb[id];
     a.P = P;
     a.nimg = n;
@@ -484,13 +547,13 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
     return a;
   };
   const int h1 = g.c1y.out, w1 = g.c1x.out, h2 = g.c2y.out, w2 = g.c2x.out;
-  TIMED(L_CONV2, launch_layer(L_CONV2, conv(L_CONV2, R[0], R[1], nullptr, h1, w1, h2, w2, g.c2y.lo, g.c2x.lo), st));
-  TIMED(L_CONV3, launch_layer(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1), st));
-  TIMED(L_CONV4, launch_layer(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1), st));
+  TIMED(L_CONV2, run_layer(c, L_CONV2, conv(L_CONV2, R[0], R[1], nullptr, h1, w1, h2, w2, g.c2y.lo, g.c2x.lo), st));
+  TIMED(L_CONV3, run_layer(c, L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1), st));
+  TIMED(L_CONV4, run_layer(c, L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1), st));
   ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);
   a8.out_u8 = latent;
   a8.out_f32_latent = prequant;
-  TIMED(L_CONV8, launch_layer(L_CONV8, a8, st));
+  TIMED(L_CONV8, run_layer(c, L_CONV8, a8, st));
   return NIC_OK;
 }
 
@@ -515,6 +578,9 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
     a.out = out;
     a.res = res;
     a.w = c->wk[id];
+    a.wx = c->wx[id];
+    a.wscale[0] = c->wscale[id][0];
+    a.wscale[1] = c->wscale[id][1];
     a.bias = c->wb[id];
     a.P = P;
     a.nimg = n;
@@ -528,11 +594,11 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   };
   ConvArgs d1 = conv(L_DCONV1, nullptr, R[1], nullptr, h8, w8, 2 * h8, 2 * w8);
   d1.in_u8 = latent;
-  TIMED(L_DCONV1, launch_layer(L_DCONV1, d1, st));
+  TIMED(L_DCONV1, run_layer(c, L_DCONV1, d1, st));
   const int h2 = 2 * h8, w2 = 2 * w8;
-  TIMED(L_DCONV5, launch_layer(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2), st));
-  TIMED(L_DCONV6, launch_layer(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2), st));
-  TIMED(L_DCONV7, launch_layer(L_DCONV7, conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2), st));
+  TIMED(L_DCONV5, run_layer(c, L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2), st));
+  TIMED(L_DCONV6, run_layer(c, L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2), st));
+  TIMED(L_DCONV7, run_layer(c, L_DCONV7, conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2), st));
   Dconv8Args a8{};
   a8.in = R[0];
   a8.out_u8 = rgb;
@@ -583,6 +649,20 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
   if (n == 0) return NIC_OK;
   if (!latent || !packed) return fail(NIC_EINVAL, "nic_unpack_latent: NULL argument");
   HIP_TRY(launch_pack(packed, latent, n, h8, w8, true, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_set_precision(nic_ctx* c, int mode) {
+  if (!c) return fail(NIC_EINVAL, "nic_set_precision: NULL ctx");
+  if (mode != NIC_PRECISION_FP32 && mode != NIC_PRECISION_F16X3)
+    return fail(NIC_EINVAL, "nic_set_precision: unknown mode %d", mode);
+  c->precision = mode;
+  return NIC_OK;
+}
+
+int nic_get_precision(nic_ctx* c, int* mode) {
+  if (!c || !mode) return fail(NIC_EINVAL, "nic_get_precision: NULL argument");
+  *mode = c->precision;
   return NIC_OK;
 }
 

@@ -21,7 +21,9 @@ struct ConvArgs {
   const float* res;       // residual, same layout as out
   uint8_t* out_u8;        // [N][OH][OW][96] latent (OUT_U8_LATENT)
   float* out_f32_latent;  // optional clipped fp32 latent, same layout as out_u8
-  const float* w;         // repacked weights [2 models][taps][Cin/8][2][Cout][4]
+  const float* w;         // fp32 path: repacked weights [2 models][taps][Cin/8][2][Cout][4]
+  const uint16_t* wx;     // f16x3 path: [2 models][taps][Cin/16][hi,lo][2][Cout][8] fp16 of w*2^k
+  float wscale[2];        // f16x3 path: 2^-k per model (exact), undoes the weight pre-scale
   const float* bias;      // [2][Cout]
   int P, nimg;            // planes (= 3 * nimg), images
   int H, W;               // input spatial dims
@@ -48,7 +50,8 @@ struct Dconv8Args {
 };
 
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
-hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);
+hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
+hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st);

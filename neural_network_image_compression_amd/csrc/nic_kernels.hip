@@ -134,7 +134,7 @@ __device__ __forceinline__ void stage_halo(float* lds, const ConvArgs& a, int p,
 // clip + quantise to the latent layout.  (oy_of, ox_of) map the tile row to output coords.
 template <int COUT, int OUT_MODE, bool RESID>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, int p, int model, int nt, const f32x16& acc,
-                                           const int* oy_of, const int* ox_of) {
+                                           const int* oy_of, const int* ox_of, float scale = 1.0f) {
   const int lane = threadIdx.x & 63;
   const int co = nt * 32 + (lane & 31);
   const float b = a.bias[model * COUT + co];
@@ -142,7 +142,8 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, int p, int model, 
   for (int r = 0; r < 16; ++r) {
     const int oy = oy_of[r], ox = ox_of[r];
     if (oy < a.OH && ox < a.OW) {
-      float v = leaky02(__fadd_rn(acc[r], b));  // Conv -> BiasAdd -> leaky_relu
+      // scale is an exact power of two (1 on the fp32 path), then Conv -> BiasAdd -> leaky_relu
+      float v = leaky02(__fadd_rn(__fmul_rn(acc[r], scale), b));
       const size_t o = (((size_t)p * a.OH + oy) * a.OW + ox) * COUT + co;
       if constexpr (RESID) v = __fadd_rn(v, a.res[o]);  // x = x + res (encoder.py:25, decoder.py:29)
       if constexpr (OUT_MODE == OUT_F32) {
@@ -330,6 +331,279 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
           store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * G::NTW + j, acc[i][j], oy, ox);
       }
       tap_base += ny * nx;
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------------------------
+// Split-f16 ("f16x3") implicit-GEMM convolution on v_mfma_f32_32x32x16_f16.
+//
+// Every fp32 operand x is split as x = hi + lo, hi = f16(x), lo = f16(x - hi) (RNE; lo may
+// be subnormal, which gfx950 keeps: float_denorm_mode_16_64 = 3).  Weights are first scaled
+// by an exact power of two 2^k per model so that max|w*2^k| <= 2^15 keeps hi and lo normal.
+// The product is a*w ~= a_hi*w_hi + a_hi*w_lo + a_lo*w_hi (three MFMAs into ONE fp32
+// accumulator; f16 x f16 products are exact in fp32, the dropped a_lo*w_lo term and the
+// rounding of lo are ~2^-22 relative), so the result matches an fp32 FMA chain to within a
+// few fp32 ulps of the sum while running on the f16 matrix pipe (16x the f32 MFMA rate).
+//
+// MFMA 32x32x16 operand maps: lane l holds A[row l&31][k = 8*(l>>5) + j] and
+// B[k = 8*(l>>5) + j][col l&31], j = 0..7.  K order inside one tap: k16 step s covers input
+// channels 16s .. 16s+15, so a lane reads 8 consecutive channels of one pixel (16 B) from
+// the hi image and 16 B from the lo image.  LDS halo: per pixel [hi: Cin f16][lo: Cin f16]
+// [16 B pad].  Weights: [model][tap][s][hi,lo][h][co][j] f16, one 16-B load per fragment.
+//
+// Waves: WM x WN x WK, each wave owns MTW M tiles (32 pixels) x NTW N tiles (32 channels);
+// its B fragments for one tap stay in registers (prefetched one tap ahead from L2) while it
+// walks its M tiles, so weight traffic is 1/MTW of the MFMA operand traffic.
+// ------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW>
+struct GeomX3 {
+  static constexpr int NWAVES = WM * WN * WK;
+  static constexpr int NTHREADS = 64 * NWAVES;
+  static_assert(CIN % 16 == 0 && COUT % 32 == 0, "channel tiling");
+  static constexpr int MT = TH * TW / 32;
+  static_assert(MT == WM * MTW && (TH * TW) % 32 == 0, "M tiling");
+  static constexpr int NT = COUT / 32;
+  static_assert(NT % WN == 0, "N tiling");
+  static constexpr int NTW = NT / WN;
+  static constexpr int HH = TR ? TH + 2 : (TH - 1) * S + KS;
+  static constexpr int HW = TR ? TW + 2 : (TW - 1) * S + KS;
+  static constexpr int PSB = CIN * 4 + 16;  // LDS bytes per halo pixel
+  static constexpr int NS = CIN / 16;       // k16 steps per tap
+  static constexpr int NTAPS = KS * KS;
+  static constexpr int HALO_BYTES = HH * HW * PSB;
+  static constexpr int RED_BYTES = (WK > 1) ? (WK - 1) * WM * WN * MTW * NTW * 1024 * 4 : 0;
+  static constexpr int LDS_BYTES = HALO_BYTES > RED_BYTES ? HALO_BYTES : RED_BYTES;
+};
+
+__device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const _Float16 h = (_Float16)v[r];
+    hi[r] = h;
+    lo[r] = (_Float16)(v[r] - (float)h);  // exact difference, then RNE to f16
+  }
+}
+
+template <int IN_MODE, int CIN, int NTHREADS>
+__device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0, int HH, int HW,
+                                              int PSB) {
+  constexpr int C4 = CIN / 4;
+  const int total = HH * HW * C4;
+  if constexpr (IN_MODE == IN_F32) {
+    const float* inp = a.in + (size_t)p * a.H * a.W * CIN;
+    for (int idx = threadIdx.x; idx < total; idx += NTHREADS) {
+      const int pix = idx / C4, c4 = idx - pix * C4;
+      const int hy = pix / HW, hx = pix - hy * HW;
+      const int gy = gy0 + hy, gx = gx0 + hx;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+        v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * CIN + c4 * 4);
+      f16x4 hi, lo;
+      split4(v, hi, lo);
+      *(f16x4*)(lds + pix * PSB + c4 * 8) = hi;
+      *(f16x4*)(lds + pix * PSB + CIN * 2 + c4 * 8) = lo;
+    }
+  } else {
+    static_assert(CIN == 32, "latent planes carry 32 channels");
+    const int n = p % a.nimg, type = p / a.nimg;
+    const uint8_t* inp = a.in_u8 + (size_t)n * a.H * a.W * 96 + type * 32;
+    for (int idx = threadIdx.x; idx < total; idx += NTHREADS) {
+      const int pix = idx >> 3, c4 = idx & 7;
+      const int hy = pix / HW, hx = pix - hy * HW;
+      const int gy = gy0 + hy, gx = gx0 + hx;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        const uint32_t q = *(const uint32_t*)(inp + ((size_t)gy * a.W + gx) * 96 + c4 * 4);
+        v[0] = c_u8_to_unit[q & 255];
+        v[1] = c_u8_to_unit[(q >> 8) & 255];
+        v[2] = c_u8_to_unit[(q >> 16) & 255];
+        v[3] = c_u8_to_unit[q >> 24];
+      }
+      f16x4 hi, lo;
+      split4(v, hi, lo);
+      *(f16x4*)(lds + pix * PSB + c4 * 8) = hi;
+      *(f16x4*)(lds + pix * PSB + CIN * 2 + c4 * 8) = lo;
+    }
+  }
+}
+
+template <int NS, int NTW, int COUT>
+__device__ __forceinline__ void load_b_x3(f16x8 (&b)[NS][2][NTW], const char* wt, int wn) {
+  // wt: this lane's base for one tap: + (((s*2 + hl)*2 + h)*COUT + co)*16 bytes
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        b[s][hl][j] = *(const f16x8*)(wt + ((s * 2 + hl) * 2 * COUT + (wn * NTW + j) * 32) * 16);
+}
+
+template <int MTW, int NTW, int NS, int CIN>
+__device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 (&b)[NS][2][NTW], const char* lds,
+                                           const int (&a_off)[MTW], int toff) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const char* ap = lds + a_off[i] + toff + s * 32;
+      const f16x8 ahi = *(const f16x8*)ap;
+      const f16x8 alo = *(const f16x8*)(ap + CIN * 2);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b[s][0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[s][1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[s][0][j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, int IN_MODE,
+          int OUT_MODE, bool RESID>
+__global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) {
+  using G = GeomX3<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW>;
+  constexpr int NS = G::NS, NTW = G::NTW;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+
+  const int p = blockIdx.y;
+  const int tile = blockIdx.x;
+  const int tyi = tile / a.tiles_x;
+  const int t0y = tyi * TH, t0x = (tile - tyi * a.tiles_x) * TW;
+  const int model = p >= a.nimg ? 1 : 0;
+  int gy0, gx0;
+  if constexpr (TR) {
+    gy0 = t0y - 1;
+    gx0 = t0x - 1;
+  } else {
+    gy0 = t0y * S - a.pad_y;
+    gx0 = t0x * S - a.pad_x;
+  }
+  stage_halo_x3<IN_MODE, CIN, G::NTHREADS>(lds, a, p, gy0, gx0, G::HH, G::HW, G::PSB);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
+  int a_off[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    const int m = (wm * MTW + i) * 32 + (lane & 31);
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+    a_off[i] = (TR ? (ty * G::HW + tx) : (ty * S * G::HW + tx * S)) * G::PSB + half * 16;
+  }
+  const char* wbase = (const char*)a.wx + (size_t)model * G::NTAPS * CIN * COUT * 4 +
+                      (half * COUT + (lane & 31)) * 16;
+  const float scale = a.wscale[model];
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+
+  f16x8 bc[NS][2][NTW], bn[NS][2][NTW];
+
+  if constexpr (!TR) {
+    const int t_begin = wk * G::NTAPS / WK, t_end = (wk + 1) * G::NTAPS / WK;
+    load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);
+    __syncthreads();
+    f32x16 acc[MTW][NTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
+    for (int t = t_begin; t < t_end; ++t) {
+      const int tn = t + 1 < t_end ? t + 1 : t;
+      load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
+      const int kh = t / KS, kw = t - (t / KS) * KS;
+      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, (kh * G::HW + kw) * G::PSB);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
+    }
+    if constexpr (WK > 1) {
+      __syncthreads();  // every wave is done with the halo before it is reused
+      float* red = (float*)lds;
+      const int grp = wm + WM * wn;
+      if (wk > 0) {
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              red[((((wk - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane] = acc[i][j][r];
+      }
+      __syncthreads();
+      if (wk > 0) return;
+#pragma unroll
+      for (int k = 1; k < WK; ++k)
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              acc[i][j][r] =
+                  __fadd_rn(acc[i][j][r], red[((((k - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane]);
+    }
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      int oy[16], ox[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        oy[r] = t0y + m / TW;
+        ox[r] = t0x + m % TW;
+      }
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], oy, ox, scale);
+    }
+  } else {
+    static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
+    load_b_x3<NS, NTW, COUT>(bc, wbase, wn);
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      const int ny = py ? 3 : 2, nx = px ? 3 : 2;
+      f32x16 acc[MTW][NTW];
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
+      for (int iy = 0; iy < ny; ++iy) {
+        for (int ix = 0; ix < nx; ++ix, ++t) {
+          const int tn = t + 1 < 25 ? t + 1 : t;
+          load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
+          mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, (iy * G::HW + ix) * G::PSB);
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+              for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        int oy[16], ox[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = (wm * MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          oy[r] = 2 * (t0y + m / TW) + py;
+          ox[r] = 2 * (t0x + m % TW) + px;
+        }
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+          store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], oy, ox, scale);
+      }
     }
   }
 }
@@ -606,6 +880,43 @@ hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st) {
       return launch_conv<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, st);
     case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tile, 4 waves along M
       return launch_conv<64, 64, 5, 2, true, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, int IN_MODE,
+          int OUT_MODE, bool RESID>
+static hipError_t launch_x3(ConvArgs a, hipStream_t st) {
+  const int gy = TR ? a.H : a.OH, gx = TR ? a.W : a.OW;
+  const int tiles_y = (gy + TH - 1) / TH;
+  a.tiles_x = (gx + TW - 1) / TW;
+  dim3 grid(tiles_y * a.tiles_x, a.P);
+  hipLaunchKernelGGL(
+      (conv_x3_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW, IN_MODE, OUT_MODE, RESID>), grid,
+      dim3(64 * WM * WN * WK), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
+  switch (id) {
+    case L_CONV2:  // 32->64 k5 s2: 8x8 tile, 2 waves split N, each 64 px x 32 co
+      return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_F32, OUT_F32, false>(a, st);
+    case L_CONV3:  // 64->64 k3 s1: 8x16 tile, 2 waves split N, each 128 px x 32 co
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
+    case L_CONV4:
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, true>(a, st);
+    case L_CONV8:  // 64->32 k5 s2 -> latent: 4x8 tile, taps split over 4 waves
+      return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_F32, OUT_U8_LATENT, false>(a, st);
+    case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
+      return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_F32, false>(a, st);
+    case L_DCONV5:
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
+    case L_DCONV6:
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, true>(a, st);
+    case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tile, 2 waves split N
+      return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
     default:
       return hipErrorInvalidValue;
   }
