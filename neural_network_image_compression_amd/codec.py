@@ -197,8 +197,8 @@ class ProClass:
 
     kind = ""
 
-    def __init__(self, device: Optional[int] = None, codec: Optional[Codec] = None):
-        self.codec = codec if codec is not None else Codec(device)
+    def __init__(self, device: Optional[int] = None, codec: Optional[Codec] = None, precision: str = "f16x3"):
+        self.codec = codec if codec is not None else Codec(device, precision=precision)
 
     def load(self, path: str) -> None:
         """utils.py:26-28: weights from ``path + 'Y'`` and ``path + 'CbCr'`` (safetensors)."""

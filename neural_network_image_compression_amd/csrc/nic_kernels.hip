@@ -444,22 +444,89 @@ __device__ __forceinline__ void load_b_x3(f16x8 (&b)[NS][2][NTW], const char* wt
         b[s][hl][j] = *(const f16x8*)(wt + ((s * 2 + hl) * 2 * COUT + (wn * NTW + j) * 32) * 16);
 }
 
+template <int MTW, int CIN>
+__device__ __forceinline__ void load_a_x3(f16x8 (&ahi)[MTW], f16x8 (&alo)[MTW], const char* lds, const int (&a_off)[MTW],
+                                          int off) {
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    ahi[i] = *(const f16x8*)(lds + a_off[i] + off);
+    alo[i] = *(const f16x8*)(lds + a_off[i] + off + CIN * 2);
+  }
+}
+
+// One tap: NS k16 steps x MTW x NTW tiles x 3 MFMAs.  The weights are the MFMA A operand
+// (rows = output channels) and the activations the B operand (columns = pixels), so the
+// accumulator holds D[co][pixel]: each lane owns one pixel and, per register group g, four
+// consecutive channels -- the epilogue then writes 16-B vectors.  A fragments are double
+// buffered: step s+1 (or step 0 of the next tap, at offset toff_next) is read while the
+// MFMAs of step s run.
 template <int MTW, int NTW, int NS, int CIN>
 __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 (&b)[NS][2][NTW], const char* lds,
-                                           const int (&a_off)[MTW], int toff) {
+                                           const int (&a_off)[MTW], int toff, int toff_next, f16x8 (&ahi0)[MTW],
+                                           f16x8 (&alo0)[MTW]) {
+  f16x8 ahi1[MTW], alo1[MTW];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
+    f16x8(&chi)[MTW] = (s & 1) ? ahi1 : ahi0;
+    f16x8(&clo)[MTW] = (s & 1) ? alo1 : alo0;
+    f16x8(&nhi)[MTW] = (s & 1) ? ahi0 : ahi1;
+    f16x8(&nlo)[MTW] = (s & 1) ? alo0 : alo1;
+    if (s + 1 < NS)
+      load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff + (s + 1) * 32);
+    else
+      load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff_next);
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) {
-      const char* ap = lds + a_off[i] + toff + s * 32;
-      const f16x8 ahi = *(const f16x8*)ap;
-      const f16x8 alo = *(const f16x8*)(ap + CIN * 2);
+    for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b[s][0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[s][1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[s][0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][1][j], chi[i], acc[i][j], 0, 0, 0);  // w_lo*a_hi
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);  // w_hi*a_lo
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], chi[i], acc[i][j], 0, 0, 0);  // w_hi*a_hi
       }
+  }
+  if constexpr (NS % 2 == 1) {  // the next tap's step 0 landed in the odd buffer
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      ahi0[i] = ahi1[i];
+      alo0[i] = alo1[i];
+    }
+  }
+}
+
+// Epilogue of one transposed accumulator tile D[co][pixel]: this lane's pixel is (oy, ox);
+// register r holds channel nt*32 + (r&3) + 8*(r>>2) + 4*half.  Conv -> *2^-k (exact) ->
+// BiasAdd -> leaky (-> + residual | -> clip, round(x*255) into the latent layout).
+template <int COUT, int OUT_MODE, bool RESID>
+__device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int model, int nt, const f32x16& acc, int oy,
+                                             int ox, float scale) {
+  if (oy >= a.OH || ox >= a.OW) return;
+  const int half = (threadIdx.x >> 5) & 1;
+  const size_t o = (((size_t)p * a.OH + oy) * a.OW + ox) * COUT;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int co = nt * 32 + 8 * g + 4 * half;
+    const f32x4 b = *(const f32x4*)(a.bias + model * COUT + co);
+    f32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[q]));
+    if constexpr (OUT_MODE == OUT_F32) {
+      if constexpr (RESID) {
+        const f32x4 rv = *(const f32x4*)(a.res + o + co);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[q]);
+      }
+      *(f32x4*)(a.out + o + co) = v;
+    } else {
+      const int n = p % a.nimg, type = p / a.nimg;
+      const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = clip01(v[q]);
+        packed |= (uint32_t)quant255(v[q]) << (8 * q);
+      }
+      *(uint32_t*)(a.out_u8 + lo) = packed;
+      if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
     }
   }
 }
@@ -484,40 +551,60 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
     gy0 = t0y * S - a.pad_y;
     gx0 = t0x * S - a.pad_x;
   }
-  stage_halo_x3<IN_MODE, CIN, G::NTHREADS>(lds, a, p, gy0, gx0, G::HH, G::HW, G::PSB);
-
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5;
   const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
-  int a_off[MTW];
+  const char* wbase = (const char*)a.wx + (size_t)model * G::NTAPS * CIN * COUT * 4 +
+                      (half * COUT + (lane & 31)) * 16;
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+  f16x8 bc[NS][2][NTW], bn[NS][2][NTW];
+  const int t_begin = TR ? 0 : wk * G::NTAPS / WK, t_end = TR ? 25 : (wk + 1) * G::NTAPS / WK;
+  load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);  // in flight during staging
+
+  stage_halo_x3<IN_MODE, CIN, G::NTHREADS>(lds, a, p, gy0, gx0, G::HH, G::HW, G::PSB);
+
+  // this lane's pixel (B-operand column) in each of its M tiles
+  int a_off[MTW], my[MTW], mx[MTW];
 #pragma unroll
   for (int i = 0; i < MTW; ++i) {
     const int m = (wm * MTW + i) * 32 + (lane & 31);
-    const int ty = m / TW, tx = m - (m / TW) * TW;
-    a_off[i] = (TR ? (ty * G::HW + tx) : (ty * S * G::HW + tx * S)) * G::PSB + half * 16;
+    my[i] = m / TW;
+    mx[i] = m - my[i] * TW;
+    a_off[i] = (TR ? (my[i] * G::HW + mx[i]) : (my[i] * S * G::HW + mx[i] * S)) * G::PSB + half * 16;
   }
-  const char* wbase = (const char*)a.wx + (size_t)model * G::NTAPS * CIN * COUT * 4 +
-                      (half * COUT + (lane & 31)) * 16;
   const float scale = a.wscale[model];
-  constexpr int TAP_BYTES = CIN * COUT * 4;
+  __syncthreads();
 
-  f16x8 bc[NS][2][NTW], bn[NS][2][NTW];
+  auto tap_off = [&](int t) {
+    if constexpr (TR) {
+      // phase-major tap order (host repack): phase ph = (py, px), halo offset (iy, ix)
+      const int ph = t < 4 ? 0 : t < 10 ? 1 : t < 16 ? 2 : 3;
+      const int base = ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16;
+      const int nx = (ph & 1) ? 3 : 2;
+      const int iy = (t - base) / nx, ix = (t - base) - ((t - base) / nx) * nx;
+      return (iy * G::HW + ix) * G::PSB;
+    } else {
+      const int kh = t / KS, kw = t - (t / KS) * KS;
+      return (kh * G::HW + kw) * G::PSB;
+    }
+  };
 
-  if constexpr (!TR) {
-    const int t_begin = wk * G::NTAPS / WK, t_end = (wk + 1) * G::NTAPS / WK;
-    load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);
-    __syncthreads();
-    f32x16 acc[MTW][NTW];
+  f16x8 ahi[MTW], alo[MTW];
+  load_a_x3<MTW, CIN>(ahi, alo, lds, a_off, tap_off(t_begin));
+
+  f32x16 acc[MTW][NTW];
+  auto zero_acc = [&]() {
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
-    for (int t = t_begin; t < t_end; ++t) {
+  };
+  auto run_taps = [&](int tb, int te) {
+    for (int t = tb; t < te; ++t) {
       const int tn = t + 1 < t_end ? t + 1 : t;
       load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
-      const int kh = t / KS, kw = t - (t / KS) * KS;
-      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, (kh * G::HW + kw) * G::PSB);
+      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, tap_off(t), tap_off(tn), ahi, alo);
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -525,6 +612,11 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 #pragma unroll
           for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
     }
+  };
+
+  if constexpr (!TR) {
+    zero_acc();
+    run_taps(t_begin, t_end);
     if constexpr (WK > 1) {
       __syncthreads();  // every wave is done with the halo before it is reused
       float* red = (float*)lds;
@@ -552,58 +644,23 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
                   __fadd_rn(acc[i][j][r], red[((((k - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane]);
     }
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) {
-      int oy[16], ox[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = (wm * MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        oy[r] = t0y + m / TW;
-        ox[r] = t0x + m % TW;
-      }
+    for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
-        store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], oy, ox, scale);
-    }
+        store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale);
   } else {
     static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
-    load_b_x3<NS, NTW, COUT>(bc, wbase, wn);
-    __syncthreads();
-    int t = 0;
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
       const int py = ph >> 1, px = ph & 1;
-      const int ny = py ? 3 : 2, nx = px ? 3 : 2;
-      f32x16 acc[MTW][NTW];
+      zero_acc();
+      run_taps(ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16, ph == 0 ? 4 : ph == 1 ? 10 : ph == 2 ? 16 : 25);
 #pragma unroll
       for (int i = 0; i < MTW; ++i)
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
-      for (int iy = 0; iy < ny; ++iy) {
-        for (int ix = 0; ix < nx; ++ix, ++t) {
-          const int tn = t + 1 < 25 ? t + 1 : t;
-          load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
-          mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, (iy * G::HW + ix) * G::PSB);
-#pragma unroll
-          for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int hl = 0; hl < 2; ++hl)
-#pragma unroll
-              for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        int oy[16], ox[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = (wm * MTW + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          oy[r] = 2 * (t0y + m / TW) + py;
-          ox[r] = 2 * (t0x + m % TW) + px;
-        }
-#pragma unroll
         for (int j = 0; j < NTW; ++j)
-          store_tile<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], oy, ox, scale);
-      }
+          store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
+                                              2 * (t0x + mx[i]) + px, scale);
     }
   }
 }

@@ -250,13 +250,13 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     ck = str(tmp_path / "ckpt" / "encoder")
     W.save(weights_spread, ck, "encoder")
     W.save(weights_spread, str(tmp_path / "ckpt" / "decoder"), "decoder")
-    enc = Encoder(0)
+    enc = Encoder(0, precision=codecs["spread"].precision)
     enc.compress(str(ds), ck)
     packed = np.array(Image.open(tmp_path / "kodak_compressed" / "img1.png"))
     assert packed.shape == (64, 128, 3)
     z = codecs["spread"].encode(_dev(g["x"][1:2])).cpu().numpy()
     np.testing.assert_array_equal(packed, O.pack_latent(z)[0])
-    dec = Decoder(0)
+    dec = Decoder(0, precision=codecs["spread"].precision)
     dec.uncompress(str(tmp_path / "kodak_compressed"), str(tmp_path / "ckpt" / "decoder"))
     rec = np.array(Image.open(tmp_path / "kodak_uncompressed" / "img1.png"))
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
