@@ -699,12 +699,13 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
-  // B fragments: W1[model][tap 0..25][co], tap 25 is zero padding
+  // Weights are the MFMA A operand (rows = output channels), the plane values the B operand
+  // (columns = pixels): lane half h supplies tap 2s+h of step s; D[co][pixel] then gives
+  // each lane one pixel and four consecutive channels per register group (16-B stores).
   float bw[13];
   const float* w = a.w + model * 26 * 32 + (lane & 31);
 #pragma unroll
   for (int s = 0; s < 13; ++s) bw[s] = w[(2 * s + half) * 32];
-  const float bias = a.bias[model * 32 + (lane & 31)];
 
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -718,48 +719,61 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
       if (tap > 24) tap = 24;  // weight is zero; any finite operand
       const int kh = tap / 5, kw = tap % 5;
       const float av = plane[(ty * 2 + kh) * C1_PS + tx * 2 + kw];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[s], av, acc, 0, 0, 0);
     }
+    const int oy = t0y + ty, ox = t0x + tx;
+    if (oy < a.OH && ox < a.OW) {
+      float* o = a.out + (((size_t)p * a.OH + oy) * a.OW + ox) * 32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mr = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const int oy = t0y + mr / C1_T, ox = t0x + mr % C1_T;
-      if (oy < a.OH && ox < a.OW)
-        a.out[(((size_t)p * a.OH + oy) * a.OW + ox) * 32 + (lane & 31)] = leaky02(__fadd_rn(acc[r], bias));
+      for (int g = 0; g < 4; ++g) {
+        const int co = 8 * g + 4 * half;
+        const f32x4 b = *(const f32x4*)(a.bias + model * 32 + co);
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(acc[4 * g + q], b[q]));
+        *(f32x4*)(o + co) = v;
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
 // dconv8 (64 -> 1, transposed k5 s2) fused with the inverse colour transform and output
-// quantiser (decoder.py:31-32, 45-48; utils.py:70-72).  One thread per coarse input
-// position computes its 4 output phases for the Y, Cb and Cr planes of one image, then
-// converts to RGB.  Cin is staged through LDS 16 channels at a time.
+// quantiser (decoder.py:31-32, 45-48; utils.py:70-72).  HBM-bound: it streams the 64-ch
+// dconv7 output once (P x 4h x 4w x 256 B) and writes 3 B per output pixel.
+// Block = 256 threads = 8 x 32 coarse positions of one image, one thread per position;
+// for each of the Y, Cb, Cr planes the 10 x 34 halo is staged 32 channels at a time
+// (128-B contiguous pieces per pixel, 144-B LDS pixel stride: conflict-free ds_read_b128 for
+// 16 consecutive positions).  A thread keeps its 4 output phases of each plane in
+// registers, then converts to RGB.  Weights are block-uniform (scalar loads).
 // ------------------------------------------------------------------------------------
-constexpr int D8_T = 16;
-constexpr int D8_HH = D8_T + 2;  // 18
-constexpr int D8_CC = 16;        // channels per LDS chunk
-constexpr int D8_PS = D8_CC + 4; // pixel stride in LDS (floats)
+constexpr int D8_TH = 8, D8_TW = 32;
+constexpr int D8_HH = D8_TH + 2, D8_HW = D8_TW + 2;  // 10 x 34
+constexpr int D8_CC = 32;                            // channels per LDS chunk
+constexpr int D8_PS = D8_CC + 4;                     // pixel stride in LDS (floats)
 
 __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
-  __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HH * D8_PS];
+  __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HW * D8_PS];
   const int n = blockIdx.y;
   const int tyi = blockIdx.x / a.tiles_x;
-  const int t0y = tyi * D8_T, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_T;
-  const int ty = threadIdx.x / D8_T, tx = threadIdx.x % D8_T;
+  const int t0y = tyi * D8_TH, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_TW;
+  const int ty = threadIdx.x / D8_TW, tx = threadIdx.x % D8_TW;
   float outv[3][4];
 
+#pragma unroll 1
   for (int type = 0; type < 3; ++type) {
     const int p = type * a.nimg + n;
     const int model = type > 0 ? 1 : 0;
     const float* inp = a.in + (size_t)p * a.H * a.W * 64;
-    const float* w = a.w + model * 25 * 64;  // [phase-tap][ci]
+    const float* __restrict__ w = a.w + model * 25 * 64;  // [phase-tap][ci]
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
     for (int c0 = 0; c0 < 64; c0 += D8_CC) {
       __syncthreads();
-      for (int idx = threadIdx.x; idx < D8_HH * D8_HH * (D8_CC / 4); idx += 256) {
-        const int pix = idx / (D8_CC / 4), c4 = idx % (D8_CC / 4);
-        const int hy = pix / D8_HH, hx = pix % D8_HH;
+      constexpr int C4 = D8_CC / 4;
+      for (int idx = threadIdx.x; idx < D8_HH * D8_HW * C4; idx += 256) {
+        const int pix = idx / C4, c4 = idx % C4;
+        const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
         const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
@@ -767,14 +781,14 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
         *(f32x4*)(halo + pix * D8_PS + c4 * 4) = v;
       }
       __syncthreads();
-#pragma unroll
+#pragma unroll 2
       for (int c4 = 0; c4 < D8_CC / 4; ++c4) {
         f32x4 x[3][3];
 #pragma unroll
         for (int iy = 0; iy < 3; ++iy)
 #pragma unroll
           for (int ix = 0; ix < 3; ++ix)
-            x[iy][ix] = *(const f32x4*)(halo + ((ty + iy) * D8_HH + tx + ix) * D8_PS + c4 * 4);
+            x[iy][ix] = *(const f32x4*)(halo + ((ty + iy) * D8_HW + tx + ix) * D8_PS + c4 * 4);
         int tb = 0;
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph) {
@@ -799,20 +813,34 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 
   const int my = t0y + ty, mx = t0x + tx;
   if (my >= a.H || mx >= a.W) return;
-  const int OH = a.H * 2, OW = a.W * 2;
+  const int OW = a.W * 2;
 #pragma unroll
-  for (int ph = 0; ph < 4; ++ph) {
-    const int oy = 2 * my + (ph >> 1), ox = 2 * mx + (ph & 1);
-    // convert_to_rgb: (Y - 0, Cb - .5, Cr - .5) projected by fp32(inv kernel), then clip
-    const float t0 = __fsub_rn(outv[0][ph], c_ycbcr_off[0]);
-    const float t1 = __fsub_rn(outv[1][ph], c_ycbcr_off[1]);
-    const float t2 = __fsub_rn(outv[2][ph], c_ycbcr_off[2]);
-    const size_t o = (((size_t)n * OH + oy) * OW + ox) * 3;
+  for (int py = 0; py < 2; ++py) {
+    // the two horizontally adjacent output pixels (2mx, 2mx+1) of row 2my+py: 6 bytes
+    uint8_t rgb[6];
+    float rgbf[6];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = clip01(project(c_ycbcr_inv + 3 * c, t0, t1, t2));
-      a.out_u8[o + c] = quant255(v);
-      if (a.out_f32) a.out_f32[o + c] = v;
+    for (int px = 0; px < 2; ++px) {
+      const int ph = py * 2 + px;
+      // convert_to_rgb: (Y - 0, Cb - .5, Cr - .5) projected by fp32(inv kernel), then clip
+      const float t0 = __fsub_rn(outv[0][ph], c_ycbcr_off[0]);
+      const float t1 = __fsub_rn(outv[1][ph], c_ycbcr_off[1]);
+      const float t2 = __fsub_rn(outv[2][ph], c_ycbcr_off[2]);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v = clip01(project(c_ycbcr_inv + 3 * c, t0, t1, t2));
+        rgbf[px * 3 + c] = v;
+        rgb[px * 3 + c] = quant255(v);
+      }
+    }
+    const size_t o = (((size_t)n * a.H * 2 + 2 * my + py) * OW + 2 * mx) * 3;
+    uint16_t* d16 = (uint16_t*)(a.out_u8 + o);  // o is even: 2-byte aligned
+    d16[0] = rgb[0] | (rgb[1] << 8);
+    d16[1] = rgb[2] | (rgb[3] << 8);
+    d16[2] = rgb[4] | (rgb[5] << 8);
+    if (a.out_f32) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
     }
   }
 }
@@ -987,8 +1015,8 @@ hipError_t launch_conv1(Conv1Args a, hipStream_t st) {
 }
 
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
-  const int tiles_y = (a.H + D8_T - 1) / D8_T;
-  a.tiles_x = (a.W + D8_T - 1) / D8_T;
+  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
+  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
   hipLaunchKernelGGL(dconv8_colour_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
