@@ -752,6 +752,25 @@ constexpr int D8_HH = D8_TH + 2, D8_HW = D8_TW + 2;  // 10 x 34
 constexpr int D8_CC = 32;                            // channels per LDS chunk
 constexpr int D8_PS = D8_CC + 4;                     // pixel stride in LDS (floats)
 
+constexpr int D8_C4 = D8_CC / 4;
+constexpr int D8_LOADS = (D8_HH * D8_HW * D8_C4 + 255) / 256;  // 16-B loads per thread per chunk
+
+// Issue the global loads of one (plane, channel chunk) halo into registers.
+__device__ __forceinline__ void d8_load(f32x4 (&r)[D8_LOADS], const Dconv8Args& a, int p, int c0, int t0y, int t0x) {
+  const float* inp = a.in + (size_t)p * a.H * a.W * 64 + c0;
+#pragma unroll
+  for (int k = 0; k < D8_LOADS; ++k) {
+    const int idx = threadIdx.x + k * 256;
+    const int pix = idx / D8_C4, c4 = idx % D8_C4;
+    const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
+    const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (idx < D8_HH * D8_HW * D8_C4 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+      v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * 64 + c4 * 4);
+    r[k] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HW * D8_PS];
   const int n = blockIdx.y;
@@ -759,56 +778,60 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   const int t0y = tyi * D8_TH, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_TW;
   const int ty = threadIdx.x / D8_TW, tx = threadIdx.x % D8_TW;
   float outv[3][4];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
 
+  // 6 steps = 3 planes (Y, Cb, Cr) x 2 channel chunks; the next step's halo is loaded
+  // into registers while this step computes (issue early, write to LDS after the barrier)
+  f32x4 pre[D8_LOADS];
+  d8_load(pre, a, n, 0, t0y, t0x);
 #pragma unroll 1
-  for (int type = 0; type < 3; ++type) {
-    const int p = type * a.nimg + n;
+  for (int step = 0; step < 6; ++step) {
+    const int type = step >> 1, c0 = (step & 1) * D8_CC;
     const int model = type > 0 ? 1 : 0;
-    const float* inp = a.in + (size_t)p * a.H * a.W * 64;
-    const float* __restrict__ w = a.w + model * 25 * 64;  // [phase-tap][ci]
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int c0 = 0; c0 < 64; c0 += D8_CC) {
-      __syncthreads();
-      constexpr int C4 = D8_CC / 4;
-      for (int idx = threadIdx.x; idx < D8_HH * D8_HW * C4; idx += 256) {
-        const int pix = idx / C4, c4 = idx % C4;
-        const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
-        const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
-          v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * 64 + c0 + c4 * 4);
-        *(f32x4*)(halo + pix * D8_PS + c4 * 4) = v;
-      }
-      __syncthreads();
+    __syncthreads();  // everyone is done reading the previous chunk
+#pragma unroll
+    for (int k = 0; k < D8_LOADS; ++k) {
+      const int idx = threadIdx.x + k * 256;
+      if (idx < D8_HH * D8_HW * D8_C4) *(f32x4*)(halo + (idx / D8_C4) * D8_PS + (idx % D8_C4) * 4) = pre[k];
+    }
+    __syncthreads();
+    if (step + 1 < 6) {
+      const int nt = (step + 1) >> 1;
+      d8_load(pre, a, nt * a.nimg + n, ((step + 1) & 1) * D8_CC, t0y, t0x);
+    }
+    const float* __restrict__ w = a.w + model * 25 * 64 + c0;  // [phase-tap][ci]
 #pragma unroll 2
-      for (int c4 = 0; c4 < D8_CC / 4; ++c4) {
-        f32x4 x[3][3];
+    for (int c4 = 0; c4 < D8_C4; ++c4) {
+      f32x4 x[3][3];
 #pragma unroll
-        for (int iy = 0; iy < 3; ++iy)
+      for (int iy = 0; iy < 3; ++iy)
 #pragma unroll
-          for (int ix = 0; ix < 3; ++ix)
-            x[iy][ix] = *(const f32x4*)(halo + ((ty + iy) * D8_HW + tx + ix) * D8_PS + c4 * 4);
-        int tb = 0;
+        for (int ix = 0; ix < 3; ++ix)
+          x[iy][ix] = *(const f32x4*)(halo + ((ty + iy) * D8_HW + tx + ix) * D8_PS + c4 * 4);
+      int tb = 0;
 #pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-          const int py = ph >> 1, px = ph & 1;
-          const int ny = py ? 3 : 2, nx = px ? 3 : 2;
+      for (int ph = 0; ph < 4; ++ph) {
+        const int py = ph >> 1, px = ph & 1;
+        const int ny = py ? 3 : 2, nx = px ? 3 : 2;
 #pragma unroll
-          for (int iy = 0; iy < ny; ++iy)
+        for (int iy = 0; iy < ny; ++iy)
 #pragma unroll
-            for (int ix = 0; ix < nx; ++ix) {
-              const float* wt = w + (tb + iy * nx + ix) * 64 + c0 + c4 * 4;
+          for (int ix = 0; ix < nx; ++ix) {
+            const float* wt = w + (tb + iy * nx + ix) * 64 + c4 * 4;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) acc[ph] = fmaf(x[iy][ix][r], wt[r], acc[ph]);
-            }
-          tb += ny * nx;
-        }
+            for (int r = 0; r < 4; ++r) acc[ph] = fmaf(x[iy][ix][r], wt[r], acc[ph]);
+          }
+        tb += ny * nx;
       }
     }
-    const float b = a.bias[model];
+    if (step & 1) {
+      const float b = a.bias[model];
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
+      for (int ph = 0; ph < 4; ++ph) {
+        outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
+        acc[ph] = 0.f;
+      }
+    }
   }
 
   const int my = t0y + ty, mx = t0x + tx;
