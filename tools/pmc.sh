@@ -22,9 +22,10 @@ while read -r group; do
   echo "[pass $i: $group] rc=$rc"
   if [ $rc -ge 124 ]; then echo "abnormal exit: stopping"; exit $rc; fi
 done <<GROUPS
-${GROUPS:-FETCH_SIZE
+${PMC_GROUPS:-FETCH_SIZE
 WRITE_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
-SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE}
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+TCC_HIT_sum TCC_MISS_sum}
 GROUPS
 exit 0
