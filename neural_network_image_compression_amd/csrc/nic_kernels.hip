@@ -367,17 +367,38 @@ struct GeomX3 {
   static_assert(CIN % 16 == 0 && COUT % 32 == 0, "channel tiling");
   static constexpr int MT = TH * TW / 32;
   static_assert(MT == WM * MTW && (TH * TW) % 32 == 0, "M tiling");
+  static_assert(TW == 8 || TW == 16 || TW % 32 == 0, "M tile = 32 pixels of 4x8, 2x16 or 1x32");
   static constexpr int NT = COUT / 32;
   static_assert(NT % WN == 0, "N tiling");
   static constexpr int NTW = NT / WN;
   static constexpr int HH = TR ? TH + 2 : (TH - 1) * S + KS;
   static constexpr int HW = TR ? TW + 2 : (TW - 1) * S + KS;
-  static constexpr int PSB = CIN * 4 + 16;  // LDS bytes per halo pixel
+  static constexpr int PSB = CIN * 4 + 16;  // LDS bytes per halo pixel: odd number of 16-B slots
+  static_assert((PSB / 16) % 2 == 1, "pixel stride must be an odd slot count");
   static constexpr int NS = CIN / 16;       // k16 steps per tap
   static constexpr int NTAPS = KS * KS;
-  static constexpr int HALO_BYTES = HH * HW * PSB;
+  // Stride-2 forward convs store even halo columns first, then odd ones, so that the 32
+  // lanes of an M tile read consecutive stored pixels for every tap.
+  static constexpr bool S2 = !TR && S == 2;
+  static constexpr int HE = S2 ? (HW + 1) / 2 : HW;
+  // Halo row pitch (16-B slots), padded so that the pitch between the rows of one M tile
+  // is 0 (TW = 16) or 8 (TW = 8) mod 16 slots: each 16-lane ds_read_b128 group then
+  // touches 16 distinct slots of the 64-bank row (conflict-free A-fragment reads).
+  static constexpr int MP_MOD = TW == 16 ? 0 : TW == 8 ? 8 : -1;
+  static constexpr int rps() {
+    int r = HW * (PSB / 16);
+    if (MP_MOD < 0) return r;
+    while (((S2 ? 2 : 1) * r) % 16 != MP_MOD) ++r;
+    return r;
+  }
+  static constexpr int RPB = rps() * 16;  // bytes per halo row
+  static constexpr int HALO_BYTES = HH * RPB;
   static constexpr int RED_BYTES = (WK > 1) ? (WK - 1) * WM * WN * MTW * NTW * 1024 * 4 : 0;
   static constexpr int LDS_BYTES = HALO_BYTES > RED_BYTES ? HALO_BYTES : RED_BYTES;
+  // LDS byte offset of halo pixel (hy, hx)
+  static __device__ __forceinline__ int pix_off(int hy, int hx) {
+    return hy * RPB + (S2 ? ((hx & 1) * HE + (hx >> 1)) : hx) * PSB;
+  }
 };
 
 __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
@@ -389,32 +410,32 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
   }
 }
 
-template <int IN_MODE, int CIN, int NTHREADS>
-__device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0, int HH, int HW,
-                                              int PSB) {
+template <class G, int IN_MODE, int CIN>
+__device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
   constexpr int C4 = CIN / 4;
-  const int total = HH * HW * C4;
+  constexpr int total = G::HH * G::HW * C4;
   if constexpr (IN_MODE == IN_F32) {
     const float* inp = a.in + (size_t)p * a.H * a.W * CIN;
-    for (int idx = threadIdx.x; idx < total; idx += NTHREADS) {
+    for (int idx = threadIdx.x; idx < total; idx += G::NTHREADS) {
       const int pix = idx / C4, c4 = idx - pix * C4;
-      const int hy = pix / HW, hx = pix - hy * HW;
+      const int hy = pix / G::HW, hx = pix - hy * G::HW;
       const int gy = gy0 + hy, gx = gx0 + hx;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
         v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * CIN + c4 * 4);
       f16x4 hi, lo;
       split4(v, hi, lo);
-      *(f16x4*)(lds + pix * PSB + c4 * 8) = hi;
-      *(f16x4*)(lds + pix * PSB + CIN * 2 + c4 * 8) = lo;
+      char* d = lds + G::pix_off(hy, hx) + c4 * 8;
+      *(f16x4*)d = hi;
+      *(f16x4*)(d + CIN * 2) = lo;
     }
   } else {
     static_assert(CIN == 32, "latent planes carry 32 channels");
     const int n = p % a.nimg, type = p / a.nimg;
     const uint8_t* inp = a.in_u8 + (size_t)n * a.H * a.W * 96 + type * 32;
-    for (int idx = threadIdx.x; idx < total; idx += NTHREADS) {
+    for (int idx = threadIdx.x; idx < total; idx += G::NTHREADS) {
       const int pix = idx >> 3, c4 = idx & 7;
-      const int hy = pix / HW, hx = pix - hy * HW;
+      const int hy = pix / G::HW, hx = pix - hy * G::HW;
       const int gy = gy0 + hy, gx = gx0 + hx;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
@@ -426,8 +447,9 @@ __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int 
       }
       f16x4 hi, lo;
       split4(v, hi, lo);
-      *(f16x4*)(lds + pix * PSB + c4 * 8) = hi;
-      *(f16x4*)(lds + pix * PSB + CIN * 2 + c4 * 8) = lo;
+      char* d = lds + G::pix_off(hy, hx) + c4 * 8;
+      *(f16x4*)d = hi;
+      *(f16x4*)(d + CIN * 2) = lo;
     }
   }
 }
@@ -562,7 +584,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   const int t_begin = TR ? 0 : wk * G::NTAPS / WK, t_end = TR ? 25 : (wk + 1) * G::NTAPS / WK;
   load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);  // in flight during staging
 
-  stage_halo_x3<IN_MODE, CIN, G::NTHREADS>(lds, a, p, gy0, gx0, G::HH, G::HW, G::PSB);
+  stage_halo_x3<G, IN_MODE, CIN>(lds, a, p, gy0, gx0);
 
   // this lane's pixel (B-operand column) in each of its M tiles
   int a_off[MTW], my[MTW], mx[MTW];
@@ -571,7 +593,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
     const int m = (wm * MTW + i) * 32 + (lane & 31);
     my[i] = m / TW;
     mx[i] = m - my[i] * TW;
-    a_off[i] = (TR ? (my[i] * G::HW + mx[i]) : (my[i] * S * G::HW + mx[i] * S)) * G::PSB + half * 16;
+    // tap (0,0) pixel of this lane: (my*S, mx*S); for S == 2 the even-column block keeps
+    // consecutive mx at consecutive stored pixels
+    a_off[i] = (TR || S == 1) ? G::pix_off(my[i], mx[i]) + half * 16
+                              : my[i] * 2 * G::RPB + mx[i] * G::PSB + half * 16;
   }
   const float scale = a.wscale[model];
   __syncthreads();
@@ -583,10 +608,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
       const int base = ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16;
       const int nx = (ph & 1) ? 3 : 2;
       const int iy = (t - base) / nx, ix = (t - base) - ((t - base) / nx) * nx;
-      return (iy * G::HW + ix) * G::PSB;
+      return iy * G::RPB + ix * G::PSB;
     } else {
       const int kh = t / KS, kw = t - (t / KS) * KS;
-      return (kh * G::HW + kw) * G::PSB;
+      return G::S2 ? kh * G::RPB + ((kw & 1) * G::HE + (kw >> 1)) * G::PSB : kh * G::RPB + kw * G::PSB;
     }
   };
 
@@ -601,6 +626,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
       for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
   };
   auto run_taps = [&](int tb, int te) {
+#pragma unroll 1
     for (int t = tb; t < te; ++t) {
       const int tn = t + 1 < t_end ? t + 1 : t;
       load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
@@ -672,7 +698,11 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 // ------------------------------------------------------------------------------------
 constexpr int C1_T = 16;
 constexpr int C1_HH = (C1_T - 1) * 2 + 5;  // 35
-constexpr int C1_PS = C1_HH + 1;           // 36 (row stride)
+constexpr int C1_HE = (C1_HH + 1) / 2;     // 18 even columns, then 17 odd ones
+// row pitch 40 dwords: the two halo rows an M tile (2 x 16 pixels, stride 2) reads per tap
+// are 80 = 16 mod 32 banks apart, and even/odd-split columns make each row's 16 reads
+// consecutive -- conflict-free ds_read_b32 for all 32 lanes of a half
+constexpr int C1_PS = 40;
 
 __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
   __shared__ float plane[C1_HH * C1_PS];
@@ -694,7 +724,7 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
       const float r = c_u8_to_unit[px[0]], g = c_u8_to_unit[px[1]], b = c_u8_to_unit[px[2]];
       v = __fadd_rn(project(k, r, g, b), off);
     }
-    plane[hy * C1_PS + hx] = v;
+    plane[hy * C1_PS + (hx & 1) * C1_HE + (hx >> 1)] = v;
   }
   __syncthreads();
 
@@ -718,7 +748,7 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
       int tap = 2 * s + half;
       if (tap > 24) tap = 24;  // weight is zero; any finite operand
       const int kh = tap / 5, kw = tap % 5;
-      const float av = plane[(ty * 2 + kh) * C1_PS + tx * 2 + kw];
+      const float av = plane[(ty * 2 + kh) * C1_PS + (kw & 1) * C1_HE + tx + (kw >> 1)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[s], av, acc, 0, 0, 0);
     }
     const int oy = t0y + ty, ox = t0x + tx;
