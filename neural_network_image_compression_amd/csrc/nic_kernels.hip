@@ -410,46 +410,62 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
   }
 }
 
+// Stage the input halo of one block into LDS as f16 hi / lo images.  Loads are issued in
+// unrolled batches of 8 from clamped (always valid) addresses and zeroed afterwards when
+// outside the image, so a batch's loads are all in flight before the first is consumed (a
+// per-element guarded load would make the compiler wait for each load separately).
 template <class G, int IN_MODE, int CIN>
 __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
   constexpr int C4 = CIN / 4;
-  constexpr int total = G::HH * G::HW * C4;
+  constexpr int TOTAL = G::HH * G::HW * C4;
+  constexpr int ITER = (TOTAL + G::NTHREADS - 1) / G::NTHREADS;
+  constexpr int BATCH = 8;
+  const float* inp = nullptr;
+  const uint8_t* inq = nullptr;
   if constexpr (IN_MODE == IN_F32) {
-    const float* inp = a.in + (size_t)p * a.H * a.W * CIN;
-    for (int idx = threadIdx.x; idx < total; idx += G::NTHREADS) {
+    inp = a.in + (size_t)p * a.H * a.W * CIN;
+  } else {
+    static_assert(CIN == 32, "latent planes carry 32 channels");
+    inq = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
+  }
+#pragma unroll
+  for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+    f32x4 v[BATCH];
+    bool inside[BATCH];
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b) {
+      if (it0 + b >= ITER) break;
+      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
       const int pix = idx / C4, c4 = idx - pix * C4;
       const int hy = pix / G::HW, hx = pix - hy * G::HW;
       const int gy = gy0 + hy, gx = gx0 + hx;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
-        v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * CIN + c4 * 4);
-      f16x4 hi, lo;
-      split4(v, hi, lo);
-      char* d = lds + G::pix_off(hy, hx) + c4 * 8;
-      *(f16x4*)d = hi;
-      *(f16x4*)(d + CIN * 2) = lo;
-    }
-  } else {
-    static_assert(CIN == 32, "latent planes carry 32 channels");
-    const int n = p % a.nimg, type = p / a.nimg;
-    const uint8_t* inp = a.in_u8 + (size_t)n * a.H * a.W * 96 + type * 32;
-    for (int idx = threadIdx.x; idx < total; idx += G::NTHREADS) {
-      const int pix = idx >> 3, c4 = idx & 7;
-      const int hy = pix / G::HW, hx = pix - hy * G::HW;
-      const int gy = gy0 + hy, gx = gx0 + hx;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-        const uint32_t q = *(const uint32_t*)(inp + ((size_t)gy * a.W + gx) * 96 + c4 * 4);
-        v[0] = c_u8_to_unit[q & 255];
-        v[1] = c_u8_to_unit[(q >> 8) & 255];
-        v[2] = c_u8_to_unit[(q >> 16) & 255];
-        v[3] = c_u8_to_unit[q >> 24];
+      inside[b] = idx < TOTAL && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+      const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+      if constexpr (IN_MODE == IN_F32) {
+        v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * CIN + c4 * 4);
+      } else {
+        const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
+        v[b][0] = c_u8_to_unit[q & 255];
+        v[b][1] = c_u8_to_unit[(q >> 8) & 255];
+        v[b][2] = c_u8_to_unit[(q >> 16) & 255];
+        v[b][3] = c_u8_to_unit[q >> 24];
       }
-      f16x4 hi, lo;
-      split4(v, hi, lo);
-      char* d = lds + G::pix_off(hy, hx) + c4 * 8;
-      *(f16x4*)d = hi;
-      *(f16x4*)(d + CIN * 2) = lo;
+    }
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b) {
+      if (it0 + b >= ITER) break;
+      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
+      if (idx < TOTAL) {
+        const int pix = idx / C4, c4 = idx - pix * C4;
+        const int hy = pix / G::HW, hx = pix - hy * G::HW;
+        f32x4 x = v[b];
+        if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
+        f16x4 hi, lo;
+        split4(x, hi, lo);
+        char* d = lds + G::pix_off(hy, hx) + c4 * 8;
+        *(f16x4*)d = hi;
+        *(f16x4*)(d + CIN * 2) = lo;
+      }
     }
   }
 }
@@ -715,16 +731,31 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
   const uint8_t* img = a.rgb + (size_t)n * a.H * a.W * 3;
   const float* k = c_ycbcr + type * 3;
   const float off = c_ycbcr_off[type];
-  for (int idx = threadIdx.x; idx < C1_HH * C1_HH; idx += 256) {
+  constexpr int C1_ITER = (C1_HH * C1_HH + 255) / 256;
+  uint8_t rgbv[C1_ITER][3];
+#pragma unroll
+  for (int it = 0; it < C1_ITER; ++it) {  // all byte loads in flight before any is used
+    const int idx = min((int)threadIdx.x + it * 256, C1_HH * C1_HH - 1);
     const int hy = idx / C1_HH, hx = idx - hy * C1_HH;
-    const int gy = gy0 + hy, gx = gx0 + hx;
-    float v = 0.f;  // SAME zero padding of the colour plane
-    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-      const uint8_t* px = img + ((size_t)gy * a.W + gx) * 3;
-      const float r = c_u8_to_unit[px[0]], g = c_u8_to_unit[px[1]], b = c_u8_to_unit[px[2]];
-      v = __fadd_rn(project(k, r, g, b), off);
+    const int cy = min(max(gy0 + hy, 0), a.H - 1), cx = min(max(gx0 + hx, 0), a.W - 1);
+    const uint8_t* px = img + ((size_t)cy * a.W + cx) * 3;
+    rgbv[it][0] = px[0];
+    rgbv[it][1] = px[1];
+    rgbv[it][2] = px[2];
+  }
+#pragma unroll
+  for (int it = 0; it < C1_ITER; ++it) {
+    const int idx = threadIdx.x + it * 256;
+    if (idx < C1_HH * C1_HH) {
+      const int hy = idx / C1_HH, hx = idx - hy * C1_HH;
+      const int gy = gy0 + hy, gx = gx0 + hx;
+      float v = 0.f;  // SAME zero padding of the colour plane
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        const float r = c_u8_to_unit[rgbv[it][0]], g = c_u8_to_unit[rgbv[it][1]], b = c_u8_to_unit[rgbv[it][2]];
+        v = __fadd_rn(project(k, r, g, b), off);
+      }
+      plane[hy * C1_PS + (hx & 1) * C1_HE + (hx >> 1)] = v;
     }
-    plane[hy * C1_PS + (hx & 1) * C1_HE + (hx >> 1)] = v;
   }
   __syncthreads();
 
@@ -794,10 +825,9 @@ __device__ __forceinline__ void d8_load(f32x4 (&r)[D8_LOADS], const Dconv8Args& 
     const int pix = idx / D8_C4, c4 = idx % D8_C4;
     const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
     const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (idx < D8_HH * D8_HW * D8_C4 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
-      v = *(const f32x4*)(inp + ((size_t)gy * a.W + gx) * 64 + c4 * 4);
-    r[k] = v;
+    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+    r[k] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * 64 + c4 * 4);  // clamped: always valid
+    if (!(gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)) r[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
 }
 
