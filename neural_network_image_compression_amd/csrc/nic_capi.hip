@@ -146,7 +146,38 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
     for_each_phase_tap([&](int t, int ky, int kx) {
       for (int ci = 0; ci < 64; ++ci) out[t * 64 + ci] = K[((size_t)(ky * 5 + kx) * 1 + 0) * 64 + ci];
     });
-    return -1000;
+    // split-f16 MFMA A fragments [nbr d=(iy,ix)][chunk c][hi,lo][lane][j]: lane l holds row
+    // l&15 (= phase (py,px) when < 4) and channels 32c + 8*(l>>4) + j.  Phase (py,px) uses
+    // halo row offset iy iff iy < 2 + py (kernel row py + 3 - 2*iy), likewise ix.
+    float maxabs = 0.f;
+    for (int i = 0; i < 25 * 64; ++i) maxabs = std::max(maxabs, std::fabs(K[i]));
+    int kexp = 0;
+    if (maxabs > 0.f && std::isfinite(maxabs)) {
+      int e = 0;
+      std::frexp(maxabs, &e);
+      kexp = std::min(std::max(15 - e, -100), 100);
+    }
+    outx.assign((size_t)9 * 2 * 2 * 64 * 8, 0);
+    for (int d = 0; d < 9; ++d) {
+      const int iy = d / 3, ix = d % 3;
+      for (int c = 0; c < 2; ++c)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row = lane & 15, kg = lane >> 4;
+          if (row >= 4) continue;
+          const int py = row >> 1, px = row & 1;
+          if (iy >= 2 + py || ix >= 2 + px) continue;
+          const int ky = py + 3 - 2 * iy, kx = px + 3 - 2 * ix;
+          for (int j = 0; j < 8; ++j) {
+            const int ci = 32 * c + 8 * kg + j;
+            const float w = std::ldexp(K[(size_t)(ky * 5 + kx) * 64 + ci], kexp);
+            const _Float16 hi = (_Float16)w;
+            const _Float16 lo = (_Float16)(w - (float)hi);
+            std::memcpy(&outx[((((size_t)d * 2 + c) * 2 + 0) * 64 + lane) * 8 + j], &hi, 2);
+            std::memcpy(&outx[((((size_t)d * 2 + c) * 2 + 1) * 64 + lane) * 8 + j], &lo, 2);
+          }
+        }
+    }
+    return kexp;
   }
   if (!L.transposed) {  // HWIO
     auto get = [&](int t, int ci, int co) { return K[((size_t)t * cin + ci) * cout + co]; };
@@ -376,13 +407,13 @@ int nic_create(int device, nic_ctx** out) {
       const LayerSpec& L = tab[i];
       const size_t kb = 2 * packed_kernel_floats(L) * sizeof(float), bb = 2 * L.cout * sizeof(float);
       if (hipMalloc(&c->wk[L.id], kb) != hipSuccess || hipMalloc(&c->wb[L.id], bb) != hipSuccess ||
-          (L.cin >= 32 && L.cout >= 32 && hipMalloc(&c->wx[L.id], kb) != hipSuccess)) {
+          (L.cin >= 32 && hipMalloc(&c->wx[L.id], L.id == L_DCONV8 ? 2 * 9 * 2 * 2 * 64 * 16 : kb) != hipSuccess)) {
         nic_destroy(c);
         return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
       }
       (void)hipMemset(c->wk[L.id], 0, kb);
       (void)hipMemset(c->wb[L.id], 0, bb);
-      if (c->wx[L.id]) (void)hipMemset(c->wx[L.id], 0, kb);
+      if (c->wx[L.id]) (void)hipMemset(c->wx[L.id], 0, L.id == L_DCONV8 ? 2 * 9 * 2 * 2 * 64 * 16 : kb);
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
     }
   }
@@ -604,11 +635,14 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   a8.out_u8 = rgb;
   a8.out_f32 = rgb_f32;
   a8.w = c->wk[L_DCONV8];
+  a8.wx = c->wx[L_DCONV8];
+  a8.wscale[0] = c->wscale[L_DCONV8][0];
+  a8.wscale[1] = c->wscale[L_DCONV8][1];
   a8.bias = c->wb[L_DCONV8];
   a8.nimg = n;
   a8.H = 2 * h2;
   a8.W = 2 * w2;
-  TIMED(L_DCONV8, launch_dconv8(a8, st));
+  TIMED(L_DCONV8, c->precision == NIC_PRECISION_F16X3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
   return NIC_OK;
 }
 

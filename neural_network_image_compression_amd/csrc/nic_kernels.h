@@ -41,11 +41,13 @@ struct Conv1Args {
 };
 
 struct Dconv8Args {
-  const float* in;   // [P][H][W][64]
-  uint8_t* out_u8;   // [N][2H][2W][3]
-  float* out_f32;    // optional clipped fp32 RGB, same layout
-  const float* w;    // [2][25 phase-taps][64]
-  const float* bias; // [2]
+  const float* in;      // [P][H][W][64]
+  uint8_t* out_u8;      // [N][2H][2W][3]
+  float* out_f32;       // optional clipped fp32 RGB, same layout
+  const float* w;       // fp32 path: [2][25 phase-taps][64]
+  const uint16_t* wx;   // f16x3 path: [2][9 nbr][2 chunk][hi,lo][64 lanes][8] MFMA A fragments
+  float wscale[2];      // f16x3 path: 2^-k per model
+  const float* bias;    // [2]
   int nimg, H, W, tiles_x;
 };
 
@@ -53,7 +55,8 @@ hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const f
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
-hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);
+hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);      // exact fp32 VALU
+hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st);   // split-f16 MFMA
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 

@@ -929,6 +929,150 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 }
 
 // ------------------------------------------------------------------------------------
+// dconv8 on the matrix pipe (split-f16, v_mfma_f32_16x16x32_f16), fused with the inverse
+// colour transform and quantiser.  Per 16 coarse positions (one row segment) and plane:
+//   D[phase][px] = sum over 9 halo neighbours d and 2 channel chunks c of A_dc x B_dc,
+//   A_dc[phase][ci] = w[tap(phase, d)][32c + ci] (0 where the phase does not use d; rows
+//   4..15 are zero), B_dc[ci][px] = x[px + d][32c + ci]
+// = 18 x 3 MFMAs.  The A fragments (weights, 36 x 16 B per lane) stay in VGPRs for a
+// whole plane; B fragments are conflict-free ds_read_b128 from 160-B pixel records
+// [hi 32 ch | lo 32 ch | pad] (10 slots: every 16-lane group hits 16 distinct slots).
+// Lanes 0..15 receive D rows 0..3 = the four phases of their pixel.
+// Block = 4 waves = 8 x 32 coarse positions of one image; wave w owns rows 2w, 2w+1.
+// ------------------------------------------------------------------------------------
+constexpr int D8M_PSB = 160;
+constexpr int D8M_HALO = D8_HH * D8_HW * D8M_PSB;  // 54,400 B
+constexpr int D8M_RES = 3 * D8_TH * D8_TW * 4 * 4;  // per-plane phase results, 12,288 B
+
+__global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
+  __shared__ __attribute__((aligned(16))) char halo[D8M_HALO + D8M_RES];
+  f32x4* res = (f32x4*)(halo + D8M_HALO);  // [plane][8 rows][32 cols] x 4 phases
+  const int n = blockIdx.y;
+  const int tyi = blockIdx.x / a.tiles_x;
+  const int t0y = tyi * D8_TH, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_TW;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  // tile i of this wave: row 2*wave + (i>>1), columns (i&1)*16 .. +15
+  int boff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    boff[i] = ((2 * wave + (i >> 1)) * D8_HW + (i & 1) * 16 + (lane & 15)) * D8M_PSB + (lane >> 4) * 16;
+
+#pragma unroll 1
+  for (int type = 0; type < 3; ++type) {
+    const int p = type * a.nimg + n;
+    const int model = type > 0 ? 1 : 0;
+    f16x8 A[9][2][2];
+    const f16x8* wa = (const f16x8*)a.wx + (size_t)model * 9 * 2 * 2 * 64 + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) A[d][c][hl] = wa[((d * 2 + c) * 2 + hl) * 64];
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const float* inp = a.in + (size_t)p * a.H * a.W * 64;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      __syncthreads();  // previous chunk fully consumed
+      constexpr int TOTAL = D8_HH * D8_HW * 8, ITER = (TOTAL + 255) / 256, BATCH = 6;
+#pragma unroll
+      for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+        f32x4 v[BATCH];
+        bool inside[BATCH];
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          if (it0 + b >= ITER) break;
+          const int idx = min((int)threadIdx.x + (it0 + b) * 256, TOTAL - 1);
+          const int pix = idx >> 3, c4 = idx & 7;
+          const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
+          const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
+          inside[b] = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+          const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+          v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * 64 + c * 32 + c4 * 4);
+        }
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          if (it0 + b >= ITER) break;
+          const int idx = threadIdx.x + (it0 + b) * 256;
+          if (idx < TOTAL) {
+            f32x4 x = v[b];
+            if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
+            f16x4 hi, lo;
+            split4(x, hi, lo);
+            char* dst = halo + (idx >> 3) * D8M_PSB + (idx & 7) * 8;
+            *(f16x4*)dst = hi;
+            *(f16x4*)(dst + 64) = lo;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int d = 0; d < 9; ++d) {
+        const int doff = ((d / 3) * D8_HW + (d % 3)) * D8M_PSB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f16x8 bhi = *(const f16x8*)(halo + boff[i] + doff);
+          const f16x8 blo = *(const f16x8*)(halo + boff[i] + doff + 64);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][1], bhi, acc[i], 0, 0, 0);  // w_lo*a_hi
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], blo, acc[i], 0, 0, 0);  // w_hi*a_lo
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], bhi, acc[i], 0, 0, 0);  // w_hi*a_hi
+        }
+      }
+    }
+    const float scale = a.wscale[model], b = a.bias[model];
+    if (lane < 16) {  // D rows 0..3 (the phases) live in lanes 0..15
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(__fadd_rn(__fmul_rn(acc[i][r], scale), b)));
+        res[(type * D8_TH + 2 * wave + (i >> 1)) * D8_TW + (i & 1) * 16 + lane] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // epilogue: one thread per coarse position, 4 output pixels x RGB
+  const int ty = threadIdx.x / D8_TW, tx = threadIdx.x % D8_TW;
+  const int my = t0y + ty, mx = t0x + tx;
+  if (my >= a.H || mx >= a.W) return;
+  const f32x4 yv = res[(0 * D8_TH + ty) * D8_TW + tx];
+  const f32x4 cbv = res[(1 * D8_TH + ty) * D8_TW + tx];
+  const f32x4 crv = res[(2 * D8_TH + ty) * D8_TW + tx];
+  const int OW = a.W * 2;
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+    uint8_t rgb[6];
+    float rgbf[6];
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      const int ph = py * 2 + px;
+      const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
+      const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
+      const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
+        rgbf[px * 3 + ch] = v;
+        rgb[px * 3 + ch] = quant255(v);
+      }
+    }
+    const size_t o = (((size_t)n * a.H * 2 + 2 * my + py) * OW + 2 * mx) * 3;
+    uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
+    d16[0] = rgb[0] | (rgb[1] << 8);
+    d16[1] = rgb[2] | (rgb[3] << 8);
+    d16[2] = rgb[4] | (rgb[5] << 8);
+    if (a.out_f32) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Histogram entropy (tf1_13/src/training.py:66-71) and bitstream pack/unpack
 // (utils.py:35-40).
 // ------------------------------------------------------------------------------------
@@ -1101,6 +1245,13 @@ hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
   const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
   a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
   hipLaunchKernelGGL(dconv8_colour_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {
+  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
+  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
+  hipLaunchKernelGGL(dconv8_x3_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
