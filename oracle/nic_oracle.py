@@ -268,3 +268,66 @@ def psnr(a: np.ndarray, b: np.ndarray, max_val: float = 255.0) -> float:
     if mse == 0:
         return float("inf")
     return float(10 * np.log10(max_val ** 2 / mse))
+
+
+# --- MS-SSIM (tf2_0/tests/calc_ssim.py:13: tf.image.ssim_multiscale(img1, img2, max_val=255)) ---
+# Restated from TensorFlow's documented algorithm (tf.image.ssim_multiscale, TF 1.13/2.0):
+# uint8 -> float32 by x * (1/255) (convert_image_dtype), max_val -> 1.0; 11x11 Gaussian
+# (sigma 1.5, softmax-normalised), VALID depthwise filtering, k1 = 0.01, k2 = 0.03;
+# 5 scales with power factors (0.0448, 0.2856, 0.3001, 0.2363, 0.1333); between scales a
+# 2x2 VALID average pool after SYMMETRIC padding of odd sizes; cs (contrast-structure) of
+# scales 0..3 and SSIM of scale 4, each relu'd, combined as a weighted geometric mean,
+# then averaged over colour channels.  Evaluated in float64 here.
+MSSSIM_WEIGHTS = (0.0448, 0.2856, 0.3001, 0.2363, 0.1333)
+
+
+def _fspecial_gauss(size: int = 11, sigma: float = 1.5) -> np.ndarray:
+    coords = np.arange(size, dtype=np.float64) - (size - 1) / 2.0
+    g = coords ** 2 * (-0.5 / sigma ** 2)
+    g = g[None, :] + g[:, None]
+    g = np.exp(g - g.max())
+    return g / g.sum()
+
+
+def _filter_valid(x: np.ndarray, k: np.ndarray) -> np.ndarray:
+    """Depthwise 'VALID' correlation of (N,H,W,C) with a separable-free (s,s) kernel."""
+    s = k.shape[0]
+    n, h, w, c = x.shape
+    out = np.zeros((n, h - s + 1, w - s + 1, c))
+    for i in range(s):
+        for j in range(s):
+            out += k[i, j] * x[:, i:i + h - s + 1, j:j + w - s + 1, :]
+    return out
+
+
+def _ssim_per_channel(x, y, max_val=1.0, k1=0.01, k2=0.03, kernel=None):
+    kernel = _fspecial_gauss() if kernel is None else kernel
+    c1, c2 = (k1 * max_val) ** 2, (k2 * max_val) ** 2
+    mean0, mean1 = _filter_valid(x, kernel), _filter_valid(y, kernel)
+    num0 = mean0 * mean1 * 2.0
+    den0 = mean0 ** 2 + mean1 ** 2
+    luminance = (num0 + c1) / (den0 + c1)
+    num1 = _filter_valid(x * y, kernel) * 2.0
+    den1 = _filter_valid(x ** 2 + y ** 2, kernel)
+    cs = (num1 - num0 + c2) / (den1 - den0 + c2)
+    return (luminance * cs).mean(axis=(1, 2)), cs.mean(axis=(1, 2))
+
+
+def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
+    """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,)."""
+    x = img1.astype(np.float64) * np.float32(1.0 / 255)
+    y = img2.astype(np.float64) * np.float32(1.0 / 255)
+    mcs = []
+    for k in range(len(MSSSIM_WEIGHTS)):
+        if k > 0:
+            h, w = x.shape[1], x.shape[2]
+            if h % 2 or w % 2:
+                pad = ((0, 0), (0, h % 2), (0, w % 2), (0, 0))
+                x, y = np.pad(x, pad, mode="symmetric"), np.pad(y, pad, mode="symmetric")
+            x = 0.25 * (x[:, 0::2, 0::2] + x[:, 1::2, 0::2] + x[:, 0::2, 1::2] + x[:, 1::2, 1::2])
+            y = 0.25 * (y[:, 0::2, 0::2] + y[:, 1::2, 0::2] + y[:, 0::2, 1::2] + y[:, 1::2, 1::2])
+        ssim_c, cs = _ssim_per_channel(x, y)
+        mcs.append(np.maximum(cs, 0))
+    mcs.pop()
+    stack = np.stack(mcs + [np.maximum(ssim_c, 0)], axis=-1)
+    return np.prod(stack ** np.asarray(MSSSIM_WEIGHTS), axis=-1).mean(axis=-1)

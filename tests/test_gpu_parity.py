@@ -6,7 +6,8 @@ Parity contract, stated per test:
   * u8 codes: identical except where the oracle's x*255 lies within 1e-3 of a .5
     rounding boundary (then +-1), and at most 0.1 % of codes;
   * decoder fed the oracle's codes: u8 |delta| <= 1 and PSNR(build, oracle) >= 50 dB;
-  * end to end: |PSNR(x, x_hat_build) - PSNR(x, x_hat_oracle)| <= 0.1 dB;
+  * end to end: |PSNR(x, x_hat_build) - PSNR(x, x_hat_oracle)| <= 0.1 dB and
+    |MS-SSIM delta| <= 1e-3 (MS-SSIM as tf2_0/tests/calc_ssim.py:13);
   * entropy: counts bit-exact, bits/symbol within 2e-6.
 Parity against TensorFlow itself is unpinned (no TF, no reference fixtures): the oracle
 stands in for it, see oracle/nic_oracle.py.
@@ -25,6 +26,7 @@ BOUNDARY = 1e-3
 MAX_FLIP_FRAC = 1e-3
 RECON_PSNR_MIN = 50.0
 E2E_PSNR_TOL = 0.1
+E2E_MSSSIM_TOL = 1e-3
 
 
 def _dev(a):
@@ -92,6 +94,7 @@ def test_end_to_end_psnr(case, codecs, golden, weights_spread):
     x = g["x"]
     r = c.decode(c.encode(_dev(x))).cpu().numpy()
     assert abs(O.psnr(x, r) - O.psnr(x, g["recon"])) <= E2E_PSNR_TOL
+    assert np.abs(O.ms_ssim(x, r) - O.ms_ssim(x, g["recon"])).max() <= E2E_MSSSIM_TOL
 
 
 @pytest.mark.parametrize("shape,seed", [((2, 24, 40), 1), ((1, 9, 17), 2), ((3, 8, 8), 3), ((1, 50, 31), 4),

@@ -152,3 +152,20 @@ def test_reference_decoder_output_size_rounds_up():
     z = O.encode(w, x)
     assert z.shape == (1, 5, 7, 96)
     assert O.decode(w, z).shape == (1, 40, 56, 3)
+
+
+def test_ms_ssim_properties(golden):
+    """MS-SSIM restatement (calc_ssim.py:13): 1 on identical images, symmetric, monotone in noise."""
+    x = golden("kodim21_256")["x"]
+    assert O.ms_ssim(x, x) == pytest.approx([1.0], abs=1e-12)
+    rng = np.random.default_rng(0)
+    prev = 1.0
+    for amp in (2, 8, 32):
+        y = np.clip(x.astype(int) + rng.integers(-amp, amp + 1, x.shape), 0, 255).astype(np.uint8)
+        s = O.ms_ssim(x, y)[0]
+        assert s < prev
+        assert s == pytest.approx(O.ms_ssim(y, x)[0], abs=1e-12)
+        prev = s
+    # gaussian window: 11 taps, sigma 1.5, normalised
+    k = O._fspecial_gauss()
+    assert k.shape == (11, 11) and k.sum() == pytest.approx(1.0) and k[5, 5] == k.max()
