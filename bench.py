@@ -105,8 +105,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="images (frames) per GPU per step")
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--workload", default="config2", choices=["config2", "kodak", "4k"],
+                    help="config2: 64 x 256^2 encode+decode (BASELINE headline); kodak: 768x512 "
+                         "whole images encode+decode (config 4 shape); 4k: 3840x2160 frames, "
+                         "encode + per-plane histogram entropy (config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="arithmetic of the Cin>=32 convolutions (see include/nic.h)")
@@ -134,20 +138,31 @@ def main():
     else:
         weights = W.seeded_weights(0)
 
-    B, S = args.batch, args.size
+    if args.workload == "config2":
+        B, H, W = args.batch or 64, args.size, args.size
+    elif args.workload == "kodak":
+        B, H, W = args.batch or 24, 512, 768
+    else:
+        B, H, W = args.batch or 8, 2160, 3840
+    S = args.size
     codec = Codec(local, precision=args.precision)
     codec.set_weights(weights)
-    codec.reserve(B, S, S)
+    codec.reserve(B, H, W)
     g = torch.Generator().manual_seed(1000 + rank)
-    x = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(device)
+    x = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8).to(device)
     from neural_network_image_compression_amd._lib import latent_shape
-    h8, w8 = latent_shape(S, S)
+    h8, w8 = latent_shape(H, W)
     z = torch.empty((B, h8, w8, 96), dtype=torch.uint8, device=device)
     r = torch.empty((B, 8 * h8, 8 * w8, 3), dtype=torch.uint8, device=device)
 
-    def step():
-        codec.encode(x, out=z)
-        codec.decode(z, out=r)
+    if args.workload == "4k":
+        def step():
+            codec.encode(x, out=z)
+            codec.entropy(z)
+    else:
+        def step():
+            codec.encode(x, out=z)
+            codec.decode(z, out=r)
 
     def barrier():
         if world > 1:
@@ -187,9 +202,11 @@ def main():
         return
 
     P = 3 * B
-    geo = layer_geometry(S, S)
+    geo = layer_geometry(H, W)
     layers = {}
     for name, (ms, n) in lt.items():
+        if n == 0:
+            continue
         avg = ms / max(n, 1)
         flop = geo[name] * P
         layers[name] = {"avg_ms": round(avg, 4), "gflop_per_launch": round(flop / 1e9, 3),
@@ -200,7 +217,7 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("batch") == B and tj.get("size") == S:
+            if tj.get("batch") == B and tj.get("size") == S and H == W == S:
                 traffic = tj["layers"].get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -211,24 +228,30 @@ def main():
                 "flop_per_launch": geo[dom] * P, "avg_launch_ms": layers[dom]["avg_ms"],
                 "peak_basis": ("dense f16 MFMA 2.5 PFLOP/s / 3 passes (algorithmic fp32 FLOP)"
                                if args.precision == "f16x3" else "dense fp32 MFMA 157.3 TFLOP/s")}
-    total_flop = sum(geo.values()) * P
+    total_flop = sum(geo[k] for k in layers) * P
     ms_step = el / args.steps * 1e3
-    value = world * B * S * S * args.steps / 1e6 / el
+    value = world * B * H * W * args.steps / 1e6 / el
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32" if args.precision == "fp32" else "fp32 (split-f16x3 MFMA)",
         "data": "synthetic",
-        "config": {"workload": f"config2: {B}x{S}x{S}x3 u8 synthetic per GPU, encode+decode (torch seed 1000+rank)",
-                   "global_batch": world * B, "image": [S, S, 3], "parallelism": f"dp{world}",
+        "config": {"workload": {"config2": f"config2: {B}x{H}x{W}x3 u8 synthetic per GPU, encode+decode",
+                                "kodak": f"config4 shape: {B}x{H}x{W}x3 whole images per GPU, encode+decode",
+                                "4k": f"config5: {B}x{H}x{W}x3 frames per GPU, encode + histogram entropy"
+                                }[args.workload] + " (torch seed 1000+rank)",
+                   "global_batch": world * B, "image": [H, W, 3], "parallelism": f"dp{world}",
                    "weights": "seeded spread init (no trained checkpoint exists)"},
         "step_tflops": round(total_flop / (ms_step * 1e-3) / 1e12, 2),
         "step_frac_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / peak, 4),
         "roofline": roofline, "layers": layers,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if args.workload == "4k":
+        out["metric"] = "Megapixels/sec encode + entropy (4K frames)"
+        out["frames_per_s"] = round(world * B * args.steps / el, 2)
+    if world == 1 and not args.no_cpu_baseline and args.workload == "config2":
         out["cpu_baseline"] = cpu_baseline(weights, S, args.cpu_seconds)
-    if not args.no_parity:
+    if not args.no_parity and args.workload == "config2":
         out["parity"] = parity_sample(codec, x[:1], weights)
     print(json.dumps(out), flush=True)
     barrier()
