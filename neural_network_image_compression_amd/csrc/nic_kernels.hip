@@ -38,6 +38,23 @@ __constant__ float c_ycbcr[9];         // fp32(ycbcr_kernel), utils.py:7
 __constant__ float c_ycbcr_inv[9];     // fp32(inv(ycbcr_kernel)), utils.py:8
 __constant__ float c_ycbcr_off[3];     // fp32(ycbcr_off), utils.py:9
 
+// Diagnostic build only (tools/stamps.cpp defines NIC_STAMPS): per-block s_memtime stamps
+// at phase boundaries of the split-f16 conv kernel.  The shipped library never records.
+#ifdef NIC_STAMPS
+__device__ unsigned long long* g_stamps;
+#define NIC_STAMP(k)                                                                         \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    if (threadIdx.x == 0)                                                                    \
+      g_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+  } while (0)
+#else
+#define NIC_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float leaky02(float z) {
   // tf.nn.leaky_relu(z, alpha=0.2) = max(alpha*z, z)
   return fmaxf(__fmul_rn(z, 0.2f), z);
@@ -578,6 +595,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 
   const int p = blockIdx.y;
   const int tile = blockIdx.x;
+  NIC_STAMP(0);
   const int tyi = tile / a.tiles_x;
   const int t0y = tyi * TH, t0x = (tile - tyi * a.tiles_x) * TW;
   const int model = p >= a.nimg ? 1 : 0;
@@ -616,6 +634,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   }
   const float scale = a.wscale[model];
   __syncthreads();
+  NIC_STAMP(1);
 
   auto tap_off = [&](int t) {
     if constexpr (TR) {
@@ -685,11 +704,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
               acc[i][j][r] =
                   __fadd_rn(acc[i][j][r], red[((((k - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane]);
     }
+    NIC_STAMP(2);
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
         store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale);
+    NIC_STAMP(3);
   } else {
     static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
 #pragma unroll
@@ -697,6 +718,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
       const int py = ph >> 1, px = ph & 1;
       zero_acc();
       run_taps(ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16, ph == 0 ? 4 : ph == 1 ? 10 : ph == 2 ? 16 : 25);
+      if (ph == 3) NIC_STAMP(2);
 #pragma unroll
       for (int i = 0; i < MTW; ++i)
 #pragma unroll
@@ -704,6 +726,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
           store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
                                               2 * (t0x + mx[i]) + px, scale);
     }
+    NIC_STAMP(3);
   }
 }
 
