@@ -428,7 +428,7 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
 }
 
 // Stage the input halo of one block into LDS as f16 hi / lo images.  Loads are issued in
-// unrolled batches of 8 from clamped (always valid) addresses and zeroed afterwards when
+// unrolled batches of 16 from clamped (always valid) addresses and zeroed afterwards when
 // outside the image, so a batch's loads are all in flight before the first is consumed (a
 // per-element guarded load would make the compiler wait for each load separately).
 template <class G, int IN_MODE, int CIN>
@@ -436,7 +436,7 @@ __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int 
   constexpr int C4 = CIN / 4;
   constexpr int TOTAL = G::HH * G::HW * C4;
   constexpr int ITER = (TOTAL + G::NTHREADS - 1) / G::NTHREADS;
-  constexpr int BATCH = 8;
+  constexpr int BATCH = 16;
   const float* inp = nullptr;
   const uint8_t* inq = nullptr;
   if constexpr (IN_MODE == IN_F32) {
@@ -552,23 +552,26 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
 // register r holds channel nt*32 + (r&3) + 8*(r>>2) + 4*half.  Conv -> *2^-k (exact) ->
 // BiasAdd -> leaky (-> + residual | -> clip, round(x*255) into the latent layout).
 template <int COUT, int OUT_MODE, bool RESID>
-__device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int model, int nt, const f32x16& acc, int oy,
-                                             int ox, float scale) {
+__device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, const f32x16& acc, int oy, int ox,
+                                             float scale, const f32x4 (&b)[4]) {
   if (oy >= a.OH || ox >= a.OW) return;
   const int half = (threadIdx.x >> 5) & 1;
   const size_t o = (((size_t)p * a.OH + oy) * a.OW + ox) * COUT;
+  f32x4 rv[4];
+  if constexpr (RESID) {  // all four residual vectors in flight before the first is used
+#pragma unroll
+    for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4*)(a.res + o + nt * 32 + 8 * g + 4 * half);
+  }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int co = nt * 32 + 8 * g + 4 * half;
-    const f32x4 b = *(const f32x4*)(a.bias + model * COUT + co);
     f32x4 v;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[q]));
+    for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[g][q]));
     if constexpr (OUT_MODE == OUT_F32) {
       if constexpr (RESID) {
-        const f32x4 rv = *(const f32x4*)(a.res + o + co);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[q]);
+        for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[g][q]);
       }
       *(f32x4*)(a.out + o + co) = v;
     } else {
@@ -614,6 +617,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   const char* wbase = (const char*)a.wx + (size_t)model * G::NTAPS * CIN * COUT * 4 +
                       (half * COUT + (lane & 31)) * 16;
   constexpr int TAP_BYTES = CIN * COUT * 4;
+  // this lane's bias vectors (channels nt*32 + 8g + 4*half .. +3), loaded up front
+  f32x4 bias4[NTW][4];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      bias4[j][g] = *(const f32x4*)(a.bias + model * COUT + (wn * NTW + j) * 32 + 8 * g + 4 * half);
   f16x8 bc[NS][2][NTW], bn[NS][2][NTW];
   const int t_begin = TR ? 0 : wk * G::NTAPS / WK, t_end = TR ? 25 : (wk + 1) * G::NTAPS / WK;
   load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);  // in flight during staging
@@ -709,7 +719,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
-        store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale);
+        store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale,
+                                            bias4[j]);
     NIC_STAMP(3);
   } else {
     static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
@@ -723,8 +734,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
       for (int i = 0; i < MTW; ++i)
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
-          store_tile_t<COUT, OUT_MODE, RESID>(a, p, model, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
-                                              2 * (t0x + mx[i]) + px, scale);
+          store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
+                                              2 * (t0x + mx[i]) + px, scale, bias4[j]);
     }
     NIC_STAMP(3);
   }

@@ -314,7 +314,11 @@ def _ssim_per_channel(x, y, max_val=1.0, k1=0.01, k2=0.03, kernel=None):
 
 
 def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
-    """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,)."""
+    """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,).
+
+    Like TF, the coarsest of the 5 scales must still hold the 11x11 window: H, W >= 176."""
+    if min(img1.shape[1], img1.shape[2]) < 11 * 2 ** (len(MSSSIM_WEIGHTS) - 1):
+        raise ValueError(f"MS-SSIM needs images of at least 176x176, got {img1.shape[1:3]}")
     x = img1.astype(np.float64) * np.float32(1.0 / 255)
     y = img2.astype(np.float64) * np.float32(1.0 / 255)
     mcs = []

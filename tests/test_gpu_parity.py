@@ -94,7 +94,8 @@ def test_end_to_end_psnr(case, codecs, golden, weights_spread):
     x = g["x"]
     r = c.decode(c.encode(_dev(x))).cpu().numpy()
     assert abs(O.psnr(x, r) - O.psnr(x, g["recon"])) <= E2E_PSNR_TOL
-    assert np.abs(O.ms_ssim(x, r) - O.ms_ssim(x, g["recon"])).max() <= E2E_MSSSIM_TOL
+    if min(x.shape[1:3]) >= 176:  # MS-SSIM's 5 scales need >= 176 px (TF asserts the same)
+        assert np.abs(O.ms_ssim(x, r) - O.ms_ssim(x, g["recon"])).max() <= E2E_MSSSIM_TOL
 
 
 @pytest.mark.parametrize("shape,seed", [((2, 24, 40), 1), ((1, 9, 17), 2), ((3, 8, 8), 3), ((1, 50, 31), 4),

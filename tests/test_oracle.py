@@ -169,3 +169,5 @@ def test_ms_ssim_properties(golden):
     # gaussian window: 11 taps, sigma 1.5, normalised
     k = O._fspecial_gauss()
     assert k.shape == (11, 11) and k.sum() == pytest.approx(1.0) and k[5, 5] == k.max()
+    with pytest.raises(ValueError):
+        O.ms_ssim(x[:, :128, :128], x[:, :128, :128])
