@@ -377,6 +377,21 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
+// NIC_PIN=1: scheduling fences so that prefetch loads (next tap's B fragments from L2, next
+// k-step's A fragments from LDS) issue before the MFMA block they overlap with; without
+// them hipcc sinks the global loads to the loop back-edge (their latency then lands on
+// the next tap's first MFMA).
+#ifndef NIC_PIN
+#define NIC_PIN 1
+#endif
+#if NIC_PIN
+#define NIC_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define NIC_FENCE() \
+  do {              \
+  } while (0)
+#endif
+
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW>
 struct GeomX3 {
   static constexpr int NWAVES = WM * WN * WK;
@@ -530,6 +545,7 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
       load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff + (s + 1) * 32);
     else
       load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff_next);
+    NIC_FENCE();
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
@@ -538,6 +554,7 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);  // w_hi*a_lo
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], chi[i], acc[i][j], 0, 0, 0);  // w_hi*a_hi
       }
+    NIC_FENCE();
   }
   if constexpr (NS % 2 == 1) {  // the next tap's step 0 landed in the odd buffer
 #pragma unroll
@@ -648,12 +665,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 
   auto tap_off = [&](int t) {
     if constexpr (TR) {
-      // phase-major tap order (host repack): phase ph = (py, px), halo offset (iy, ix)
-      const int ph = t < 4 ? 0 : t < 10 ? 1 : t < 16 ? 2 : 3;
-      const int base = ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16;
-      const int nx = (ph & 1) ? 3 : 2;
-      const int iy = (t - base) / nx, ix = (t - base) - ((t - base) / nx) * nx;
-      return iy * G::RPB + ix * G::PSB;
+      // phase-major tap order (host repack): phase ph = (py, px) has 2|3 x 2|3 halo
+      // offsets (iy, ix), one byte per tap: iy | ix << 2.  Taps 0..3: (0,0)(0,1)(1,0)(1,1);
+      // 4..9: rows 0..1 x cols 0..2; 10..15: rows 0..2 x cols 0..1; 16..24: 3x3.
+      constexpr unsigned char tab[25] = {0x0, 0x4, 0x1, 0x5, 0x0, 0x4, 0x8, 0x1, 0x5, 0x9, 0x0, 0x4, 0x1,
+                                         0x5, 0x2, 0x6, 0x0, 0x4, 0x8, 0x1, 0x5, 0x9, 0x2, 0x6, 0xa};
+      const int e = tab[t];
+      return (e & 3) * G::RPB + (e >> 2) * G::PSB;
     } else {
       const int kh = t / KS, kw = t - (t / KS) * KS;
       return G::S2 ? kh * G::RPB + ((kw & 1) * G::HE + (kw >> 1)) * G::PSB : kh * G::RPB + kw * G::PSB;
@@ -670,18 +688,28 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
   };
+  // Taps [tb, te): bc holds tap tb's B fragments on entry and tap te's (clamped) on exit.
+  // Two B buffers ping-pong; each tap's successor is requested before its MFMAs.
   auto run_taps = [&](int tb, int te) {
 #pragma unroll 1
-    for (int t = tb; t < te; ++t) {
-      const int tn = t + 1 < t_end ? t + 1 : t;
-      load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)tn * TAP_BYTES, wn);
-      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, tap_off(t), tap_off(tn), ahi, alo);
+    for (int t = tb; t < te; t += 2) {
+      const int t1 = t + 1 < t_end ? t + 1 : t_end - 1;
+      const int t2 = t + 2 < t_end ? t + 2 : t_end - 1;
+      load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)t1 * TAP_BYTES, wn);
+      NIC_FENCE();
+      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, tap_off(t), tap_off(t1), ahi, alo);
+      if (t + 1 < te) {
+        load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t2 * TAP_BYTES, wn);
+        NIC_FENCE();
+        mma_tap_x3<MTW, NTW, NS, CIN>(acc, bn, lds, a_off, tap_off(t1), tap_off(t2), ahi, alo);
+      } else {
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int hl = 0; hl < 2; ++hl)
+          for (int hl = 0; hl < 2; ++hl)
 #pragma unroll
-          for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
+            for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
+      }
     }
   };
 
