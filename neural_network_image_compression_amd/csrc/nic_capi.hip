@@ -234,6 +234,7 @@ struct nic_ctx {
   uint16_t* wx[L_COUNT] = {};  // split-f16 kernels [2 models][taps*cin*cout*2]
   float wscale[L_COUNT][2] = {};  // 2^-k per model for the split-f16 kernels
   int precision = NIC_PRECISION_F16X3;
+  char* zero16 = nullptr;  // 256 zero bytes: DMA source for halo padding
   bool have_k[4][5] = {};
   bool have_b[4][5] = {};
   char* ws = nullptr;
@@ -417,6 +418,10 @@ int nic_create(int device, nic_ctx** out) {
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
     }
   }
+  if (hipMalloc(&c->zero16, 256) != hipSuccess || hipMemset(c->zero16, 0, 256) != hipSuccess) {
+    nic_destroy(c);
+    return fail(NIC_ENOMEM, "nic_create: zero buffer allocation failed");
+  }
   // constants: u8 -> fp32 /255 (correctly rounded on the host), colour matrices
   // (utils.py:7-9; the inverse is np.linalg.inv in float64, then rounded to fp32)
   float lut[256];
@@ -443,6 +448,7 @@ int nic_destroy(nic_ctx* c) {
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
+  if (c->zero16) (void)hipFree(c->zero16);
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
@@ -544,6 +550,7 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
   Conv1Args a1{};
   a1.rgb = rgb;
   a1.out = R[0];
+  a1.out_s = c->precision == NIC_PRECISION_F16X3 ? (uint16_t*)R[0] : nullptr;
   a1.w = c->wk[L_CONV1];
   a1.bias = c->wb[L_CONV1];
   a1.P = P;
@@ -562,6 +569,10 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
     a.in = in;
     a.out = out;
     a.res = res;
+    a.in_s = (const uint16_t*)in;  // the same region read as split f16 (f16x3 kernels)
+    a.out_s = (uint16_t*)out;
+    a.res_s = (const uint16_t*)res;
+    a.zero16 = c->zero16;
     a.w = c->wk[id];
     a.wx = c->wx[id];
     a.wscale[0] = c->wscale[id][0];
@@ -608,6 +619,10 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
     a.in = in;
     a.out = out;
     a.res = res;
+    a.in_s = (const uint16_t*)in;  // the same region read as split f16 (f16x3 kernels)
+    a.out_s = (uint16_t*)out;
+    a.res_s = (const uint16_t*)res;
+    a.zero16 = c->zero16;
     a.w = c->wk[id];
     a.wx = c->wx[id];
     a.wscale[0] = c->wscale[id][0];
@@ -632,6 +647,8 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   TIMED(L_DCONV7, run_layer(c, L_DCONV7, conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2), st));
   Dconv8Args a8{};
   a8.in = R[0];
+  a8.in_s = (const uint16_t*)R[0];
+  a8.zero16 = c->zero16;
   a8.out_u8 = rgb;
   a8.out_f32 = rgb_f32;
   a8.w = c->wk[L_DCONV8];

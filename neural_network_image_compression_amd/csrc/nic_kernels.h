@@ -5,8 +5,11 @@
 
 namespace nic {
 
-enum InMode { IN_F32 = 0, IN_U8_LATENT = 1 };
-enum OutMode { OUT_F32 = 0, OUT_U8_LATENT = 1 };
+// Activation formats in HBM: fp32 NHWC (exact-fp32 mode) or "split" NHWC: per pixel
+// [hi: C f16][lo: C f16] with x = hi + lo, hi = f16(x), lo = f16(x - hi) (f16x3 mode; the
+// same 4 B per element, split once by the producer's epilogue).
+enum InMode { IN_F32 = 0, IN_U8_LATENT = 1, IN_SPLIT = 2 };
+enum OutMode { OUT_F32 = 0, OUT_U8_LATENT = 1, OUT_SPLIT = 2 };
 
 enum LayerId {
   L_CONV1 = 0, L_CONV2, L_CONV3, L_CONV4, L_CONV8,
@@ -19,6 +22,10 @@ struct ConvArgs {
   const uint8_t* in_u8;   // [N][H][W][96] latent (IN_U8_LATENT)
   float* out;             // [P][OH][OW][Cout] fp32 (OUT_F32)
   const float* res;       // residual, same layout as out
+  const uint16_t* in_s;   // [P][H][W][2][Cin] split f16 (IN_SPLIT)
+  uint16_t* out_s;        // [P][OH][OW][2][Cout] split f16 (OUT_SPLIT)
+  const uint16_t* res_s;  // residual in split format
+  const char* zero16;     // >= 16 zero bytes in global memory (DMA source for padding)
   uint8_t* out_u8;        // [N][OH][OW][96] latent (OUT_U8_LATENT)
   float* out_f32_latent;  // optional clipped fp32 latent, same layout as out_u8
   const float* w;         // fp32 path: repacked weights [2 models][taps][Cin/8][2][Cout][4]
@@ -34,14 +41,17 @@ struct ConvArgs {
 
 struct Conv1Args {
   const uint8_t* rgb;  // [N][H][W][3]
-  float* out;          // [P][OH][OW][32]
+  float* out;          // [P][OH][OW][32] fp32 (exact mode)
+  uint16_t* out_s;     // [P][OH][OW][2][32] split f16 (f16x3 mode), used when non-null
   const float* w;      // [2][26][32]
   const float* bias;   // [2][32]
   int P, nimg, H, W, OH, OW, pad_y, pad_x, tiles_x;
 };
 
 struct Dconv8Args {
-  const float* in;      // [P][H][W][64]
+  const float* in;      // [P][H][W][64] fp32 (exact mode)
+  const uint16_t* in_s; // [P][H][W][2][64] split f16 (f16x3 mode)
+  const char* zero16;   // DMA padding source
   uint8_t* out_u8;      // [N][2H][2W][3]
   float* out_f32;       // optional clipped fp32 RGB, same layout
   const float* w;       // fp32 path: [2][25 phase-taps][64]

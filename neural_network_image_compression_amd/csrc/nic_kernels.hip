@@ -424,7 +424,8 @@ struct GeomX3 {
     return r;
   }
   static constexpr int RPB = rps() * 16;  // bytes per halo row
-  static constexpr int HALO_BYTES = HH * RPB;
+  // DMA staging writes whole 64-slot wave-instructions: round the image up to them
+  static constexpr int HALO_BYTES = (HH * RPB + 1023) / 1024 * 1024;
   static constexpr int RED_BYTES = (WK > 1) ? (WK - 1) * WM * WN * MTW * NTW * 1024 * 4 : 0;
   static constexpr int LDS_BYTES = HALO_BYTES > RED_BYTES ? HALO_BYTES : RED_BYTES;
   // LDS byte offset of halo pixel (hy, hx)
@@ -446,6 +447,39 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
 // unrolled batches of 16 from clamped (always valid) addresses and zeroed afterwards when
 // outside the image, so a batch's loads are all in flight before the first is consumed (a
 // per-element guarded load would make the compiler wait for each load separately).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+// One 16-B direct-to-LDS load per lane (global_load_lds_dwordx4): lane l of the wave writes
+// LDS bytes [wave_base + 16*l, +16).  No VGPR destination, counted in vmcnt.
+__device__ __forceinline__ void dma16(const char* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Stage a split-format halo by DMA: every 16-B slot of the LDS image (pixel records of
+// PSB bytes, padded rows) is one lane-load; record slot k < Cin/4 copies slot k of the
+// pixel's [hi | lo] record in HBM, the pad slot, row padding and out-of-image pixels load
+// zeros.  One HBM round trip per block, no VGPR staging, no conversion.
+template <class G, int CIN>
+__device__ __forceinline__ void stage_halo_dma(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
+  constexpr int PSS = G::PSB / 16, RPS = G::RPB / 16;
+  constexpr int TOTAL = G::HH * RPS;
+  const char* base = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#pragma unroll 4
+  for (int q0 = wave * 64; q0 < TOTAL; q0 += G::NTHREADS) {
+    const int q = q0 + lane;
+    const int row = q / RPS, r = q - row * RPS;
+    const int sp = r / PSS, k = r - sp * PSS;
+    const int hx = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
+    const int gy = gy0 + row, gx = gx0 + hx;
+    const bool valid = q < TOTAL && sp < G::HW && k < PSS - 1 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+    const char* src = valid ? base + ((size_t)gy * a.W + gx) * (CIN * 4) + k * 16 : a.zero16;
+    dma16(src, lds + q0 * 16);
+  }
+}
+
 template <class G, int IN_MODE, int CIN>
 __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
   constexpr int C4 = CIN / 4;
@@ -573,11 +607,21 @@ __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, c
                                              float scale, const f32x4 (&b)[4]) {
   if (oy >= a.OH || ox >= a.OW) return;
   const int half = (threadIdx.x >> 5) & 1;
-  const size_t o = (((size_t)p * a.OH + oy) * a.OW + ox) * COUT;
+  const size_t pix = ((size_t)p * a.OH + oy) * a.OW + ox;
   f32x4 rv[4];
-  if constexpr (RESID) {  // all four residual vectors in flight before the first is used
+  if constexpr (RESID) {  // all residual vectors in flight before the first is used
 #pragma unroll
-    for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4*)(a.res + o + nt * 32 + 8 * g + 4 * half);
+    for (int g = 0; g < 4; ++g) {
+      const int co = nt * 32 + 8 * g + 4 * half;
+      if constexpr (OUT_MODE == OUT_SPLIT) {  // residual stored split: x = hi + lo
+        const f16x4 h = *(const f16x4*)(a.res_s + pix * COUT * 2 + co);
+        const f16x4 l = *(const f16x4*)(a.res_s + pix * COUT * 2 + COUT + co);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rv[g][q] = __fadd_rn((float)h[q], (float)l[q]);
+      } else {
+        rv[g] = *(const f32x4*)(a.res + pix * COUT + co);
+      }
+    }
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -585,12 +629,17 @@ __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, c
     f32x4 v;
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[g][q]));
-    if constexpr (OUT_MODE == OUT_F32) {
-      if constexpr (RESID) {
+    if constexpr (RESID) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[g][q]);
-      }
-      *(f32x4*)(a.out + o + co) = v;
+      for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[g][q]);
+    }
+    if constexpr (OUT_MODE == OUT_F32) {
+      *(f32x4*)(a.out + pix * COUT + co) = v;
+    } else if constexpr (OUT_MODE == OUT_SPLIT) {
+      f16x4 hi, lo;
+      split4(v, hi, lo);
+      *(f16x4*)(a.out_s + pix * COUT * 2 + co) = hi;
+      *(f16x4*)(a.out_s + pix * COUT * 2 + COUT + co) = lo;
     } else {
       const int n = p % a.nimg, type = p / a.nimg;
       const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co;
@@ -645,7 +694,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   const int t_begin = TR ? 0 : wk * G::NTAPS / WK, t_end = TR ? 25 : (wk + 1) * G::NTAPS / WK;
   load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);  // in flight during staging
 
-  stage_halo_x3<G, IN_MODE, CIN>(lds, a, p, gy0, gx0);
+  if constexpr (IN_MODE == IN_SPLIT)
+    stage_halo_dma<G, CIN>(lds, a, p, gy0, gx0);
+  else
+    stage_halo_x3<G, IN_MODE, CIN>(lds, a, p, gy0, gx0);
 
   // this lane's pixel (B-operand column) in each of its M tiles
   int a_off[MTW], my[MTW], mx[MTW];
@@ -660,6 +712,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
                               : my[i] * 2 * G::RPB + mx[i] * G::PSB + half * 16;
   }
   const float scale = a.wscale[model];
+  if constexpr (IN_MODE == IN_SPLIT) dma_wait_all();  // this wave's DMAs landed; barrier publishes all
   __syncthreads();
   NIC_STAMP(1);
 
@@ -846,7 +899,7 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
     }
     const int oy = t0y + ty, ox = t0x + tx;
     if (oy < a.OH && ox < a.OW) {
-      float* o = a.out + (((size_t)p * a.OH + oy) * a.OW + ox) * 32;
+      const size_t pix = ((size_t)p * a.OH + oy) * a.OW + ox;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int co = 8 * g + 4 * half;
@@ -854,7 +907,14 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
         f32x4 v;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(acc[4 * g + q], b[q]));
-        *(f32x4*)(o + co) = v;
+        if (a.out_s) {  // split format for the f16x3 conv2
+          f16x4 hi, lo;
+          split4(v, hi, lo);
+          *(f16x4*)(a.out_s + pix * 64 + co) = hi;
+          *(f16x4*)(a.out_s + pix * 64 + 32 + co) = lo;
+        } else {
+          *(f32x4*)(a.out + pix * 32 + co) = v;
+        }
       }
     }
   }
@@ -1003,7 +1063,7 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 // Block = 4 waves = 8 x 32 coarse positions of one image; wave w owns rows 2w, 2w+1.
 // ------------------------------------------------------------------------------------
 constexpr int D8M_PSB = 160;
-constexpr int D8M_HALO = D8_HH * D8_HW * D8M_PSB;  // 54,400 B
+constexpr int D8M_HALO = (D8_HH * D8_HW * D8M_PSB + 4095) / 4096 * 4096;  // whole DMA rounds (57,344 B)
 constexpr int D8M_RES = 3 * D8_TH * D8_TW * 4 * 4;  // per-plane phase results, 12,288 B
 
 __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
@@ -1035,41 +1095,25 @@ __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
     f32x4 acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const float* inp = a.in + (size_t)p * a.H * a.W * 64;
+    const char* inb = (const char*)a.in_s + (size_t)p * a.H * a.W * 256;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       __syncthreads();  // previous chunk fully consumed
-      constexpr int TOTAL = D8_HH * D8_HW * 8, ITER = (TOTAL + 255) / 256, BATCH = 6;
-#pragma unroll
-      for (int it0 = 0; it0 < ITER; it0 += BATCH) {
-        f32x4 v[BATCH];
-        bool inside[BATCH];
-#pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          if (it0 + b >= ITER) break;
-          const int idx = min((int)threadIdx.x + (it0 + b) * 256, TOTAL - 1);
-          const int pix = idx >> 3, c4 = idx & 7;
-          const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
-          const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
-          inside[b] = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-          const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-          v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * 64 + c * 32 + c4 * 4);
-        }
-#pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          if (it0 + b >= ITER) break;
-          const int idx = threadIdx.x + (it0 + b) * 256;
-          if (idx < TOTAL) {
-            f32x4 x = v[b];
-            if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
-            f16x4 hi, lo;
-            split4(x, hi, lo);
-            char* dst = halo + (idx >> 3) * D8M_PSB + (idx & 7) * 8;
-            *(f16x4*)dst = hi;
-            *(f16x4*)(dst + 64) = lo;
-          }
-        }
+      // DMA the 10 x 34 halo of channel chunk c: record slots 0..3 <- hi slots 4c..4c+3,
+      // 4..7 <- lo slots 8+4c.., 8..9 <- zeros; out-of-image pixels <- zeros
+      constexpr int SLOTS = D8_HH * D8_HW * 10;
+#pragma unroll 2
+      for (int q0 = wave * 64; q0 < SLOTS; q0 += 256) {
+        const int q = q0 + lane;
+        const int pix = q / 10, k = q - pix * 10;
+        const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
+        const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
+        const bool valid = q < SLOTS && k < 8 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+        const int gslot = k < 4 ? 4 * c + k : 8 + 4 * c + (k - 4);
+        const char* src = valid ? inb + ((size_t)gy * a.W + gx) * 256 + gslot * 16 : a.zero16;
+        dma16(src, halo + q0 * 16);
       }
+      dma_wait_all();
       __syncthreads();
 #pragma unroll
       for (int d = 0; d < 9; ++d) {
@@ -1276,21 +1320,21 @@ static hipError_t launch_x3(ConvArgs a, hipStream_t st) {
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
     case L_CONV2:  // 32->64 k5 s2: 8x8 tile, 2 waves split N, each 64 px x 32 co
-      return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_F32, OUT_F32, false>(a, st);
+      return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV3:  // 64->64 k3 s1: 8x16 tile, 2 waves split N, each 128 px x 32 co
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV4:
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, true>(a, st);
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, true>(a, st);
     case L_CONV8:  // 64->32 k5 s2 -> latent: 4x8 tile, taps split over 4 waves
-      return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_F32, OUT_U8_LATENT, false>(a, st);
+      return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_SPLIT, OUT_U8_LATENT, false>(a, st);
     case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
-      return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_F32, false>(a, st);
+      return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
     case L_DCONV5:
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_DCONV6:
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, true>(a, st);
+      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, true>(a, st);
     case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tile, 2 waves split N
-      return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_F32, OUT_F32, false>(a, st);
+      return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     default:
       return hipErrorInvalidValue;
   }

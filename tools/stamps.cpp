@@ -69,11 +69,18 @@ int main() {
     CK(hipMemcpy(wx, hw.data(), wn * 2, hipMemcpyHostToDevice));
     CK(hipMemset(bias, 0, 2 * c.cout * 4));
     CK(hipMemset(in8, 7, (size_t)N * c.H * c.W * 96));
+    char* zero16;
+    CK(hipMalloc(&zero16, 256));
+    CK(hipMemset(zero16, 0, 256));
     ConvArgs a{};
     a.in = in;
+    a.in_s = (const uint16_t*)in;
+    a.zero16 = zero16;
     a.in_u8 = in8;
     a.out = out;
+    a.out_s = (uint16_t*)out;
     a.res = c.resid ? res : nullptr;
+    a.res_s = (const uint16_t*)res;
     a.out_u8 = out8;
     a.wx = wx;
     a.wscale[0] = a.wscale[1] = 1.f;
@@ -124,6 +131,7 @@ int main() {
     CK(hipFree(out8));
     CK(hipFree(wx));
     CK(hipFree(st));
+    CK(hipFree(zero16));
   }
   return 0;
 }
