@@ -14,7 +14,8 @@ import threading
 from typing import List, Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnic.so")
+# NIC_LIB: load another build of the same C-ABI (A/B comparisons of kernel variants)
+LIB_PATH = os.environ.get("NIC_LIB") or os.path.join(HERE, "libnic.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "nic.h")
 
 LAYER_NAMES = ("conv1", "conv2", "conv3", "conv4", "conv8", "dconv1", "dconv5", "dconv6", "dconv7", "dconv8")

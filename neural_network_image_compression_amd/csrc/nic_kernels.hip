@@ -455,7 +455,28 @@ typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 __device__ __forceinline__ void dma16(const char* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
 }
-__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(0) through the builtin (simm16 0x0F70: vmcnt 0, expcnt 7, lgkmcnt 15) so hipcc's
+// counter model sees the LDS-DMA drained; behind inline asm it would keep treating the DMA
+// as pending and wait vmcnt(0) before every later LDS read, draining the B prefetches.
+__device__ __forceinline__ void dma_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// Split-format 16-B stores from a transposed accumulator: per register group g a lane
+// owns channels 8g + 4*half .. +3 of its pixel.  permlane32_swap exchanges group pairs
+// (g, g+1) between the lane halves so that lanes 0..31 hold channels 8g..8g+7 and lanes
+// 32..63 channels 8g+8..8g+15 (cdna_hip_programming.md T21); the inverse map is the same
+// swap.  a, b: this lane's two dwords of groups g and g+1 (f16x4 each).
+__device__ __forceinline__ void swap_pair(f16x4& a, f16x4& b) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto r = __builtin_amdgcn_permlane32_swap(ua[d], ub[d], false, false);
+    ua[d] = r[0];
+    ub[d] = r[1];
+  }
+  a = __builtin_bit_cast(f16x4, ua);
+  b = __builtin_bit_cast(f16x4, ub);
+}
 
 // Stage a split-format halo by DMA: every 16-B slot of the LDS image (pixel records of
 // PSB bytes, padded rows) is one lane-load; record slot k < Cin/4 copies slot k of the
@@ -605,52 +626,81 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
 template <int COUT, int OUT_MODE, bool RESID>
 __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, const f32x16& acc, int oy, int ox,
                                              float scale, const f32x4 (&b)[4]) {
-  if (oy >= a.OH || ox >= a.OW) return;
+  const bool inside = oy < a.OH && ox < a.OW;
   const int half = (threadIdx.x >> 5) & 1;
-  const size_t pix = ((size_t)p * a.OH + oy) * a.OW + ox;
+  const size_t pix = ((size_t)p * (inside ? a.OH : 1) + (inside ? oy : 0)) * (inside ? a.OW : 1) + (inside ? ox : 0);
+  f32x4 v[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[g][q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[g][q]));
+  if constexpr (OUT_MODE == OUT_SPLIT) {
+    // every lane takes part in the swaps (EXEC must stay full); only in-image lanes store
+    uint16_t* base = a.out_s + pix * COUT * 2 + nt * 32;
+    const uint16_t* rbase = a.res_s + pix * COUT * 2 + nt * 32;
+    f16x8 rh[2] = {}, rl[2] = {};
+    if constexpr (RESID) {  // residual stored split: x = hi + lo; all four 16-B loads in flight
+      if (inside) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          rh[k] = *(const f16x8*)(rbase + 16 * k + 8 * half);
+          rl[k] = *(const f16x8*)(rbase + COUT + 16 * k + 8 * half);
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const int co = 8 * g + 8 * half;  // channel block this lane stores after the swap
+      if constexpr (RESID) {  // inverse swap back to the accumulator's channel map
+        const f16x8 &r = rh[g >> 1], &q = rl[g >> 1];
+        f16x4 h0 = {r[0], r[1], r[2], r[3]}, h1 = {r[4], r[5], r[6], r[7]};
+        f16x4 l0 = {q[0], q[1], q[2], q[3]}, l1 = {q[4], q[5], q[6], q[7]};
+        swap_pair(h0, h1);
+        swap_pair(l0, l1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          v[g][c] = __fadd_rn(v[g][c], __fadd_rn((float)h0[c], (float)l0[c]));
+          v[g + 1][c] = __fadd_rn(v[g + 1][c], __fadd_rn((float)h1[c], (float)l1[c]));
+        }
+      }
+      f16x4 h0, l0, h1, l1;
+      split4(v[g], h0, l0);
+      split4(v[g + 1], h1, l1);
+      swap_pair(h0, h1);
+      swap_pair(l0, l1);
+      if (inside) {
+        *(f16x8*)(base + co) = (f16x8){h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        *(f16x8*)(base + COUT + co) = (f16x8){l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      }
+    }
+    return;
+  }
+  if (!inside) return;
   f32x4 rv[4];
   if constexpr (RESID) {  // all residual vectors in flight before the first is used
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int co = nt * 32 + 8 * g + 4 * half;
-      if constexpr (OUT_MODE == OUT_SPLIT) {  // residual stored split: x = hi + lo
-        const f16x4 h = *(const f16x4*)(a.res_s + pix * COUT * 2 + co);
-        const f16x4 l = *(const f16x4*)(a.res_s + pix * COUT * 2 + COUT + co);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rv[g][q] = __fadd_rn((float)h[q], (float)l[q]);
-      } else {
-        rv[g] = *(const f32x4*)(a.res + pix * COUT + co);
-      }
-    }
+    for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4*)(a.res + pix * COUT + nt * 32 + 8 * g + 4 * half);
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int co = nt * 32 + 8 * g + 4 * half;
-    f32x4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[g][q]));
     if constexpr (RESID) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = __fadd_rn(v[q], rv[g][q]);
+      for (int q = 0; q < 4; ++q) v[g][q] = __fadd_rn(v[g][q], rv[g][q]);
     }
     if constexpr (OUT_MODE == OUT_F32) {
-      *(f32x4*)(a.out + pix * COUT + co) = v;
-    } else if constexpr (OUT_MODE == OUT_SPLIT) {
-      f16x4 hi, lo;
-      split4(v, hi, lo);
-      *(f16x4*)(a.out_s + pix * COUT * 2 + co) = hi;
-      *(f16x4*)(a.out_s + pix * COUT * 2 + COUT + co) = lo;
+      *(f32x4*)(a.out + pix * COUT + co) = v[g];
     } else {
       const int n = p % a.nimg, type = p / a.nimg;
       const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co;
       uint32_t packed = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v[q] = clip01(v[q]);
-        packed |= (uint32_t)quant255(v[q]) << (8 * q);
+        v[g][q] = clip01(v[g][q]);
+        packed |= (uint32_t)quant255(v[g][q]) << (8 * q);
       }
       *(uint32_t*)(a.out_u8 + lo) = packed;
-      if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
+      if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v[g];
     }
   }
 }
@@ -719,11 +769,12 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   auto tap_off = [&](int t) {
     if constexpr (TR) {
       // phase-major tap order (host repack): phase ph = (py, px) has 2|3 x 2|3 halo
-      // offsets (iy, ix), one byte per tap: iy | ix << 2.  Taps 0..3: (0,0)(0,1)(1,0)(1,1);
-      // 4..9: rows 0..1 x cols 0..2; 10..15: rows 0..2 x cols 0..1; 16..24: 3x3.
-      constexpr unsigned char tab[25] = {0x0, 0x4, 0x1, 0x5, 0x0, 0x4, 0x8, 0x1, 0x5, 0x9, 0x0, 0x4, 0x1,
-                                         0x5, 0x2, 0x6, 0x0, 0x4, 0x8, 0x1, 0x5, 0x9, 0x2, 0x6, 0xa};
-      const int e = tab[t];
+      // offsets (iy, ix), one nibble per tap: iy | ix << 2.  Taps 0..3: (0,0)(0,1)(1,0)(1,1);
+      // 4..9: rows 0..1 x cols 0..2; 10..15: rows 0..2 x cols 0..1; 16..24: 3x3.  The table
+      // lives in two 64-bit immediates: t is wave-uniform, so this is a few SALU shifts; an
+      // array would be a global_load_ubyte whose vmcnt wait drains the B prefetch in flight.
+      constexpr unsigned long long kTabLo = 0x6251409518405140ull, kTabHi = 0x0000000a62951840ull;
+      const int e = (int)((t < 16 ? kTabLo >> (4 * t) : kTabHi >> (4 * (t - 16))) & 15);
       return (e & 3) * G::RPB + (e >> 2) * G::PSB;
     } else {
       const int kh = t / KS, kw = t - (t / KS) * KS;
@@ -898,24 +949,32 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[s], av, acc, 0, 0, 0);
     }
     const int oy = t0y + ty, ox = t0x + tx;
-    if (oy < a.OH && ox < a.OW) {
-      const size_t pix = ((size_t)p * a.OH + oy) * a.OW + ox;
+    const bool inside = oy < a.OH && ox < a.OW;
+    const size_t pix = inside ? ((size_t)p * a.OH + oy) * a.OW + ox : 0;
+    f32x4 v[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co = 8 * g + 4 * half;
-        const f32x4 b = *(const f32x4*)(a.bias + model * 32 + co);
-        f32x4 v;
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b = *(const f32x4*)(a.bias + model * 32 + 8 * g + 4 * half);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = leaky02(__fadd_rn(acc[4 * g + q], b[q]));
-        if (a.out_s) {  // split format for the f16x3 conv2
-          f16x4 hi, lo;
-          split4(v, hi, lo);
-          *(f16x4*)(a.out_s + pix * 64 + co) = hi;
-          *(f16x4*)(a.out_s + pix * 64 + 32 + co) = lo;
-        } else {
-          *(f32x4*)(a.out + pix * 32 + co) = v;
+      for (int q = 0; q < 4; ++q) v[g][q] = leaky02(__fadd_rn(acc[4 * g + q], b[q]));
+    }
+    if (a.out_s) {  // split format for the f16x3 conv2: 16-B stores after lane-half swaps
+#pragma unroll
+      for (int g = 0; g < 4; g += 2) {
+        f16x4 h0, l0, h1, l1;
+        split4(v[g], h0, l0);
+        split4(v[g + 1], h1, l1);
+        swap_pair(h0, h1);
+        swap_pair(l0, l1);
+        const int co = 8 * g + 8 * half;
+        if (inside) {
+          *(f16x8*)(a.out_s + pix * 64 + co) = (f16x8){h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+          *(f16x8*)(a.out_s + pix * 64 + 32 + co) = (f16x8){l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
         }
       }
+    } else if (inside) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) *(f32x4*)(a.out + pix * 32 + 8 * g + 4 * half) = v[g];
     }
   }
 }
