@@ -8,7 +8,7 @@ namespace nic {
 // Activation formats in HBM: fp32 NHWC (exact-fp32 mode) or "split" NHWC: per pixel
 // [hi: C f16][lo: C f16] with x = hi + lo, hi = f16(x), lo = f16(x - hi) (f16x3 mode; the
 // same 4 B per element, split once by the producer's epilogue).
-enum InMode { IN_F32 = 0, IN_U8_LATENT = 1, IN_SPLIT = 2 };
+enum InMode { IN_F32 = 0, IN_U8_LATENT = 1, IN_SPLIT = 2, IN_SPLIT_DMA = 3 };
 enum OutMode { OUT_F32 = 0, OUT_U8_LATENT = 1, OUT_SPLIT = 2 };
 
 enum LayerId {
@@ -37,6 +37,7 @@ struct ConvArgs {
   int OH, OW;             // output spatial dims
   int pad_y, pad_x;       // forward conv TF-SAME pad_lo
   int tiles_x;            // set by the launcher
+  int tiles_y, ntiles;    // pipelined kernels: tile grid (set by the launcher)
 };
 
 struct Conv1Args {

@@ -1,0 +1,40 @@
+"""Child-process parity check of the opt-in pipelined kernels (NIC_PIPE=1 is read once when
+libnic.so loads, so it cannot be toggled inside the pytest process).  Run by
+tests/test_gpu_parity.py::test_pipelined_kernels_parity; applies the same contract as the
+golden encode/decode tests there (prequant atol, codes, recon) and prints PIPE-OK."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402  (HIP runtime before libnic.so)
+
+from conftest import load_case  # noqa: E402
+from neural_network_image_compression_amd import weights as W  # noqa: E402
+from neural_network_image_compression_amd.codec import Codec  # noqa: E402
+from oracle import nic_oracle as O  # noqa: E402
+from test_gpu_parity import PREQUANT_ATOL, check_codes, check_recon  # noqa: E402
+
+
+def main():
+    assert os.environ.get("NIC_PIPE") == "1"
+    c = Codec(0, precision="f16x3")
+    c.set_weights(W.seeded_weights(0, init="spread"))
+    for case in ("kodim21_256", "imagenet4", "odd37x53"):
+        g = load_case(case)
+        z, f = c.encode(torch.from_numpy(g["x"]).cuda(), prequant=True)
+        z, f = z.cpu().numpy(), f.cpu().numpy()
+        assert np.abs(f - g["prequant"]).max() <= PREQUANT_ATOL, case
+        check_codes(z, g["latent"], g["prequant"])
+        r = c.decode(torch.from_numpy(g["latent"]).cuda()).cpu().numpy()
+        check_recon(r, g["recon"])
+        np.testing.assert_array_equal(O.quantise_u8(f), z)
+    print("PIPE-OK")
+
+
+if __name__ == "__main__":
+    main()
