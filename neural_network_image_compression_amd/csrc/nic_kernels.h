@@ -38,6 +38,7 @@ struct ConvArgs {
   int pad_y, pad_x;       // forward conv TF-SAME pad_lo
   int tiles_x;            // set by the launcher
   int tiles_y, ntiles;    // pipelined kernels: tile grid (set by the launcher)
+  int nblk_y;             // weight-stationary kernels: blocks serving the Y model
 };
 
 struct Conv1Args {

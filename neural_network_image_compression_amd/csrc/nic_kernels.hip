@@ -1298,6 +1298,151 @@ __global__ __launch_bounds__(64 * (NCW + NPW)) void conv_pipe_kernel(ConvArgs a)
 }
 
 // ------------------------------------------------------------------------------------
+// Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16), stride-1 k3.
+// Wave w owns output channels 16w .. 16w+15 and keeps their weights for every tap and
+// input channel in VGPRs (the MFMA A operand: w_hi and w_lo, 9 x 2 k32-steps x 2 = 36
+// fragments = 144 VGPRs), loaded once per block.  Blocks serve one model (Y or CbCr) and
+// loop over its tiles, so no weight byte is re-read per tile: the one-tile-per-block
+// kernels move ~8 KB of weight fragments per wave and tap through L2.  The halo of tile
+// i+1 is DMA'd into the other LDS buffer by all waves while tile i's MFMAs run; the
+// epilogue of tile i runs after the next barrier so its stores overlap tile i+1.
+// D[co][pixel] per 16-pixel tile (two 8-pixel rows): lane (g, l16) holds channels
+// 16w + 4g .. +3 of pixel l16.
+// ------------------------------------------------------------------------------------
+template <int CIN, int COUT, int TH, int TW, bool RESID>
+__global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
+  constexpr int KS = 3, NTAPS = 9, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
+  static_assert(TW == 8 && CIN % 32 == 0 && COUT % 16 == 0, "16-pixel tiles = two 8-pixel rows");
+  using G = GeomX3<CIN, COUT, KS, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
+  using HP = HaloPieces<G, CIN, CIN, NW>;
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES];
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int co0 = wave * 16 + 4 * g;  // this lane's 4 output channels
+  // blocks [0, nblk_y) serve the Y planes' tiles (the first nimg planes), the rest CbCr
+  const int per_plane = a.tiles_y * a.tiles_x, n_y = a.nimg * per_plane;
+  const int blk = blockIdx.x, nb_y = a.nblk_y, nb_c = gridDim.x - nb_y;
+  const int model = blk < nb_y ? 0 : 1;
+  const int first = model ? n_y + (blk - nb_y) : blk, stride = model ? nb_c : nb_y;
+  const int end = model ? a.ntiles : n_y;
+  const int ntile = first < end ? (end - first + stride - 1) / stride : 0;
+
+  // resident weights: A fragment (row co = 16w + l16, k = 8g + j of k32-step ks) is the
+  // f16x3 repack's 16-B chunk (k16-step 2ks + g/2, half g%2) of channel 16w + l16
+  f16x8 wr[NTAPS][KST][2];
+  {
+    const char* wsrc = (const char*)a.wx + (size_t)model * NTAPS * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          wr[t][ks][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
+                                          ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + wave * 16 + l16) * 16);
+  }
+  const float scale = a.wscale[model];
+  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
+
+  // B-fragment base of each 16-pixel tile: pixel (2m + l16/8, l16%8), channels 8g..8g+7
+  int boff[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) boff[m] = G::pix_off(2 * m + (l16 >> 3), l16 & 7) + g * 16;
+
+  HP hp;
+  hp.init(wave, lane);
+  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
+    const int t = first + i * stride;
+    p = t / per_plane;
+    const int r = t - p * per_plane, ty = r / a.tiles_x;
+    t0y = ty * TH;
+    t0x = (r - ty * a.tiles_x) * TW;
+  };
+  auto issue = [&](int i) {
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    hp.issue(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4, a.zero16, a.H,
+             a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
+  };
+
+  f32x4 acc[MT];
+  f16x4 rhi[MT], rlo[MT];  // split residual of the tile in flight (RESID)
+  int ep_p = 0, ep_y = 0, ep_x = 0;  // tile whose epilogue is pending
+  if (ntile > 0) issue(0);
+  for (int i = 0; i <= ntile; ++i) {
+    dma_wait_all();  // this wave's DMAs of tile i (and the residual loads of tile i-1)
+    lds_reads_done();
+    stage_barrier();  // tile i's halo complete; everyone is done reading tile i-1's buffer
+    if (i > 0) {  // epilogue of tile i-1: *2^-k, bias, leaky (+ residual), split, 8-B stores
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int oy = ep_y + 2 * m + (l16 >> 3), ox = ep_x + (l16 & 7);
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
+          if constexpr (RESID) v[r] = __fadd_rn(v[r], __fadd_rn((float)rhi[m][r], (float)rlo[m][r]));
+        }
+        f16x4 hi, lo;
+        split4(v, hi, lo);
+        if (oy < a.OH && ox < a.OW) {
+          uint16_t* o = a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + co0;
+          *(f16x4*)o = hi;
+          *(f16x4*)(o + COUT) = lo;
+        }
+      }
+    }
+    if (i == ntile) break;
+    if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
+    tile_at(i, ep_p, ep_y, ep_x);
+    if constexpr (RESID) {  // consumed by this tile's epilogue, after the next vmcnt(0)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int oy = min(ep_y + 2 * m + (l16 >> 3), a.OH - 1), ox = min(ep_x + (l16 & 7), a.OW - 1);
+        const uint16_t* r = a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + co0;
+        rhi[m] = *(const f16x4*)r;
+        rlo[m] = *(const f16x4*)(r + COUT);
+      }
+    }
+    const char* buf = lds + (i & 1) * G::HALO_BYTES;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // 9 taps x KST k32-steps, fully unrolled (the weight registers are indexed statically).
+    // Rolling fragment buffer: once pixel tile m's three MFMAs of step s are issued, its
+    // registers receive step s+1's fragment, (MT-1)*3 MFMAs before they are needed.
+    constexpr int NSTEP = NTAPS * KST;
+    f16x8 fb[MT][2];
+    auto step_off = [&](int st) {
+      const int t = st / KST, ks = st - t * KST, kh = t / KS, kw = t - kh * KS;
+      return kh * G::RPB + kw * G::PSB + ks * 64;
+    };
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      fb[m][0] = *(const f16x8*)(buf + boff[m] + step_off(0));
+      fb[m][1] = *(const f16x8*)(buf + boff[m] + step_off(0) + CIN * 2);
+    }
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      const int t = st / KST, ks = st - t * KST;
+      const int noff = step_off(st + 1 < NSTEP ? st + 1 : st);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
+        if (st + 1 < NSTEP) {
+          fb[m][0] = *(const f16x8*)(buf + boff[m] + noff);
+          fb[m][1] = *(const f16x8*)(buf + boff[m] + noff + CIN * 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
 // utils.py:74-77).  Block: 16x16 output pixels of one plane, 4 waves x 2 M tiles x 32 co.
 // K = 25 taps padded to 26 (13 MFMAs); lane half h supplies tap 2s+h of step s.
@@ -1842,6 +1987,16 @@ static bool use_pipe() {
   return on;
 }
 
+// NIC_WS=0 selects the one-tile-per-block kernels for the 3x3 layers instead of the
+// weight-stationary ones (A/B)
+static bool use_ws() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_WS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int device_cus() {
   static int cache[64] = {};
   int d = 0;
@@ -1870,15 +2025,34 @@ static hipError_t launch_pipe(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int CIN, int COUT, int TH, int TW, bool RESID>
+static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
+  a.tiles_y = (a.OH + TH - 1) / TH;
+  a.tiles_x = (a.OW + TW - 1) / TW;
+  const long long nt = (long long)a.tiles_y * a.tiles_x * a.P;
+  if (nt == 0) return hipSuccess;
+  if (nt > INT32_MAX || a.P != 3 * a.nimg) return hipErrorInvalidValue;
+  a.ntiles = (int)nt;
+  // two resident blocks per CU; a third of them serve the Y planes (a third of the tiles)
+  int grid = 2 * device_cus();
+  if (grid > a.ntiles) grid = a.ntiles;
+  if (grid < 2) grid = 2;
+  a.nblk_y = grid / 3 > 0 ? grid / 3 : 1;
+  hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID>), dim3(grid), dim3(64 * (COUT / 16)), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
     case L_CONV2:  // 32->64 k5 s2: 8x8 tile, 2 waves split N, each 64 px x 32 co
       return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
                    // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
+      if (use_ws()) return launch_ws<64, 64, 8, 8, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV4:
+      if (use_ws()) return launch_ws<64, 64, 8, 8, true>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
     case L_CONV8:  // 64->32 k5 s2 -> latent: 4x8 tile, taps split over 4 waves
@@ -1886,9 +2060,11 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
     case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
       return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
     case L_DCONV5:
+      if (use_ws()) return launch_ws<64, 64, 8, 8, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_DCONV6:
+      if (use_ws()) return launch_ws<64, 64, 8, 8, true>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
     case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tiles (one stage each), 4 consumers x 32 px x 64 co

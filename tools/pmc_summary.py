@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first match)
-    (r"conv1_colour", "conv1"), (r"dconv8_colour", "dconv8"),
+    (r"conv1_colour", "conv1"), (r"dconv8_colour", "dconv8"), (r"dconv8_x3", "dconv8"),
     (r"<32, 64, 5, 2, false", "conv2"), (r"<64, 32, 5, 2, false", "conv8"),
     (r"<32, 64, 5, 2, true", "dconv1"), (r"<64, 64, 5, 2, true", "dconv7"),
     (r"<64, 64, 3, 1, false.*true>", "k3_resid"), (r"<64, 64, 3, 1, false.*false>", "k3"),
@@ -61,6 +61,15 @@ def main():
             d["hbm_bytes_per_launch"] = int((2 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024)
         if "SQ_LDS_BANK_CONFLICT" in med and "SQ_LDS_IDX_ACTIVE" in med and med["SQ_LDS_IDX_ACTIVE"] > 0:
             d["lds_bank_conflict_frac"] = med["SQ_LDS_BANK_CONFLICT"] / med["SQ_LDS_IDX_ACTIVE"]
+        wc = med.get("SQ_WAVE_CYCLES", 0)
+        if wc > 0:  # disjoint wave-state buckets (guide: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES)
+            for c, k in (("SQ_WAIT_ANY", "wave_waitcnt_barrier_frac"), ("SQ_WAIT_INST_ANY", "wave_issue_stall_frac"),
+                         ("SQ_ACTIVE_INST_ANY", "wave_issuing_frac")):
+                if c in med:
+                    d[k] = med[c] / wc
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in med and med.get("GRBM_GUI_ACTIVE", 0) > 0:
+            # per-SIMD MFMA busy fraction: counter summed over 256 CUs x 4 SIMDs, GRBM in GPU cycles
+            d["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * med["GRBM_GUI_ACTIVE"] / 8)
         summary[lay] = d
     # the k3 kernels serve conv3/dconv5 and conv4/dconv6
     for a, b in (("k3", ("conv3", "dconv5")), ("k3_resid", ("conv4", "dconv6"))):
