@@ -38,7 +38,9 @@ struct ConvArgs {
   int pad_y, pad_x;       // forward conv TF-SAME pad_lo
   int tiles_x;            // set by the launcher
   int tiles_y, ntiles;    // pipelined kernels: tile grid (set by the launcher)
-  int nblk_y;             // weight-stationary kernels: blocks serving the Y model
+  int ws_taps;            // weight-stationary kernels: taps per model in wx
+  int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
+  int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
 };
 
 struct Conv1Args {

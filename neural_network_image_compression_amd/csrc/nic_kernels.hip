@@ -1298,42 +1298,46 @@ __global__ __launch_bounds__(64 * (NCW + NPW)) void conv_pipe_kernel(ConvArgs a)
 }
 
 // ------------------------------------------------------------------------------------
-// Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16), stride-1 k3.
-// Wave w owns output channels 16w .. 16w+15 and keeps their weights for every tap and
-// input channel in VGPRs (the MFMA A operand: w_hi and w_lo, 9 x 2 k32-steps x 2 = 36
-// fragments = 144 VGPRs), loaded once per block.  Blocks serve one model (Y or CbCr) and
-// loop over its tiles, so no weight byte is re-read per tile: the one-tile-per-block
-// kernels move ~8 KB of weight fragments per wave and tap through L2.  The halo of tile
-// i+1 is DMA'd into the other LDS buffer by all waves while tile i's MFMAs run; the
-// epilogue of tile i runs after the next barrier so its stores overlap tile i+1.
+// Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16) over a
+// stride-1 window of KH x KW taps: the k3 s1 layers (KH = KW = 3), and each of the four
+// sub-pixel phases of the k5 s2 Conv2DTranspose dconv7 (2x2, 2x3, 3x2, 3x3 taps, TRP).
+// Wave w owns output channels 16w .. 16w+15 and keeps their weights for every tap of its
+// window and every input channel in VGPRs (the MFMA A operand: w_hi and w_lo, at most
+// 9 x 2 k32-steps x 2 = 36 fragments = 144 VGPRs), loaded once per block.  A launch is cut
+// into block groups, one per (tap set, model); a group's blocks loop over that model's
+// tiles, so no weight byte is re-read per tile (the one-tile-per-block kernels move ~8 KB
+// of weight fragments per wave and tap through L2).  The halo of tile i+1 is DMA'd into
+// the other LDS buffer by all waves while tile i's MFMAs run; the epilogue of tile i runs
+// after the next barrier so its stores overlap tile i+1.
 // D[co][pixel] per 16-pixel tile (two 8-pixel rows): lane (g, l16) holds channels
-// 16w + 4g .. +3 of pixel l16.
+// 16w + 4g .. +3 of pixel l16.  Phase (py, px) of a transposed layer writes fine pixel
+// (2y + py, 2x + px) for coarse position (y, x), from halo taps (iy, ix) < (KH, KW) at
+// origin (y - 1, x - 1) with weight tap tb + iy * KW + ix (host phase-major repack).
 // ------------------------------------------------------------------------------------
-template <int CIN, int COUT, int TH, int TW, bool RESID>
-__global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
-  constexpr int KS = 3, NTAPS = 9, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
+template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP>
+__device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
+                                        int px) {
+  constexpr int NTAPS = KH * KW, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
   static_assert(TW == 8 && CIN % 32 == 0 && COUT % 16 == 0, "16-pixel tiles = two 8-pixel rows");
-  using G = GeomX3<CIN, COUT, KS, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
+  static_assert(!(TRP && RESID), "no residual on the transposed phases");
+  using G = GeomX3<CIN, COUT, 3, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
   using HP = HaloPieces<G, CIN, CIN, NW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES];
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   const int co0 = wave * 16 + 4 * g;  // this lane's 4 output channels
-  // blocks [0, nblk_y) serve the Y planes' tiles (the first nimg planes), the rest CbCr
-  const int per_plane = a.tiles_y * a.tiles_x, n_y = a.nimg * per_plane;
-  const int blk = blockIdx.x, nb_y = a.nblk_y, nb_c = gridDim.x - nb_y;
-  const int model = blk < nb_y ? 0 : 1;
-  const int first = model ? n_y + (blk - nb_y) : blk, stride = model ? nb_c : nb_y;
-  const int end = model ? a.ntiles : n_y;
-  const int ntile = first < end ? (end - first + stride - 1) / stride : 0;
+  // this group's tiles: the planes of `model` ([0, nimg) Y, [nimg, P) CbCr), block bi of nb
+  const int per_plane = a.tiles_y * a.tiles_x;
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  const int ntot = np * per_plane;
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
 
   // resident weights: A fragment (row co = 16w + l16, k = 8g + j of k32-step ks) is the
   // f16x3 repack's 16-B chunk (k16-step 2ks + g/2, half g%2) of channel 16w + l16
   f16x8 wr[NTAPS][KST][2];
   {
-    const char* wsrc = (const char*)a.wx + (size_t)model * NTAPS * TAP_BYTES;
+    const char* wsrc = (const char*)a.wx + ((size_t)model * a.ws_taps + tb) * TAP_BYTES;
 #pragma unroll
     for (int t = 0; t < NTAPS; ++t)
 #pragma unroll
@@ -1354,9 +1358,10 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
   HP hp;
   hp.init(wave, lane);
   auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
-    const int t = first + i * stride;
-    p = t / per_plane;
-    const int r = t - p * per_plane, ty = r / a.tiles_x;
+    const int t = bi + i * nb;
+    const int pl = t / per_plane;
+    p = p0 + pl;
+    const int r = t - pl * per_plane, ty = r / a.tiles_x;
     t0y = ty * TH;
     t0x = (r - ty * a.tiles_x) * TW;
   };
@@ -1378,7 +1383,7 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
     if (i > 0) {  // epilogue of tile i-1: *2^-k, bias, leaky (+ residual), split, 8-B stores
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const int oy = ep_y + 2 * m + (l16 >> 3), ox = ep_x + (l16 & 7);
+        const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1387,7 +1392,8 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
         }
         f16x4 hi, lo;
         split4(v, hi, lo);
-        if (oy < a.OH && ox < a.OW) {
+        if (y < a.H && x < a.W) {
+          const int oy = TRP ? 2 * y + py : y, ox = TRP ? 2 * x + px : x;
           uint16_t* o = a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + co0;
           *(f16x4*)o = hi;
           *(f16x4*)(o + COUT) = lo;
@@ -1409,13 +1415,13 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
     const char* buf = lds + (i & 1) * G::HALO_BYTES;
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // 9 taps x KST k32-steps, fully unrolled (the weight registers are indexed statically).
+    // NTAPS x KST k32-steps, fully unrolled (the weight registers are indexed statically).
     // Rolling fragment buffer: once pixel tile m's three MFMAs of step s are issued, its
     // registers receive step s+1's fragment, (MT-1)*3 MFMAs before they are needed.
     constexpr int NSTEP = NTAPS * KST;
     f16x8 fb[MT][2];
     auto step_off = [&](int st) {
-      const int t = st / KST, ks = st - t * KST, kh = t / KS, kw = t - kh * KS;
+      const int t = st / KST, ks = st - t * KST, kh = t / KW, kw = t - kh * KW;
       return kh * G::RPB + kw * G::PSB + ks * 64;
     };
 #pragma unroll
@@ -1438,6 +1444,28 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
       }
+    }
+  }
+}
+
+// Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi & 1, tap set gi >> 1
+// (the phase of a transposed layer).
+template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
+__global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
+  using G = GeomX3<CIN, COUT, 3, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES];
+  int gi = 0;
+  while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
+  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int model = gi & 1;
+  if constexpr (!TRP) {
+    ws_body<CIN, COUT, TH, TW, RESID, 3, 3, false>(a, lds, model, bi, nb, 0, 0, 0);
+  } else {
+    switch (gi >> 1) {  // phase-major tap bases 0, 4, 10, 16 (for_each_phase_tap)
+      case 0: ws_body<CIN, COUT, TH, TW, false, 2, 2, true>(a, lds, model, bi, nb, 0, 0, 0); break;
+      case 1: ws_body<CIN, COUT, TH, TW, false, 2, 3, true>(a, lds, model, bi, nb, 4, 0, 1); break;
+      case 2: ws_body<CIN, COUT, TH, TW, false, 3, 2, true>(a, lds, model, bi, nb, 10, 1, 0); break;
+      default: ws_body<CIN, COUT, TH, TW, false, 3, 3, true>(a, lds, model, bi, nb, 16, 1, 1); break;
     }
   }
 }
@@ -2025,20 +2053,37 @@ static hipError_t launch_pipe(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int CIN, int COUT, int TH, int TW, bool RESID>
+// Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
+// in proportion to each group's MFMA work (planes x taps).
+template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
 static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
-  a.tiles_y = (a.OH + TH - 1) / TH;
-  a.tiles_x = (a.OW + TW - 1) / TW;
-  const long long nt = (long long)a.tiles_y * a.tiles_x * a.P;
+  a.tiles_y = (a.H + TH - 1) / TH;
+  a.tiles_x = (a.W + TW - 1) / TW;
+  const long long per_plane = (long long)a.tiles_y * a.tiles_x;
+  const long long nt = per_plane * a.P;
   if (nt == 0) return hipSuccess;
   if (nt > INT32_MAX || a.P != 3 * a.nimg) return hipErrorInvalidValue;
   a.ntiles = (int)nt;
-  // two resident blocks per CU; a third of them serve the Y planes (a third of the tiles)
-  int grid = 2 * device_cus();
-  if (grid > a.ntiles) grid = a.ntiles;
-  if (grid < 2) grid = 2;
-  a.nblk_y = grid / 3 > 0 ? grid / 3 : 1;
-  hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID>), dim3(grid), dim3(64 * (COUT / 16)), 0, st, a);
+  const int nset = TRP ? 4 : 1;
+  const int taps[4] = {TRP ? 4 : 9, 6, 6, 9};
+  a.ws_taps = TRP ? 25 : 9;
+  a.ws_ngrp = 2 * nset;
+  long long work[8], total = 0;
+  for (int gi = 0; gi < a.ws_ngrp; ++gi) {
+    const long long planes = (gi & 1) ? a.P - a.nimg : a.nimg;
+    work[gi] = planes * per_plane * taps[gi >> 1];
+    total += work[gi];
+  }
+  const int target = 2 * device_cus();
+  a.ws_blk[0] = 0;
+  for (int gi = 0; gi < a.ws_ngrp; ++gi) {
+    const long long tiles = ((gi & 1) ? a.P - a.nimg : a.nimg) * per_plane;
+    long long b = (work[gi] * target + total / 2) / total;
+    b = b < 1 ? 1 : b > tiles ? tiles : b;
+    a.ws_blk[gi + 1] = a.ws_blk[gi] + (int)b;
+  }
+  hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP>), dim3(a.ws_blk[a.ws_ngrp]), dim3(64 * (COUT / 16)),
+                     0, st, a);
   return hipGetLastError();
 }
 
@@ -2048,11 +2093,11 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
       return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
                    // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
-      if (use_ws()) return launch_ws<64, 64, 8, 8, false>(a, st);
+      if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV4:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, true>(a, st);
+      if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
     case L_CONV8:  // 64->32 k5 s2 -> latent: 4x8 tile, taps split over 4 waves
@@ -2060,14 +2105,15 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
     case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
       return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
     case L_DCONV5:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, false>(a, st);
+      if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_DCONV6:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, true>(a, st);
+      if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
-    case L_DCONV7:  // 64->64 transposed k5 s2: 8x16 coarse tiles (one stage each), 4 consumers x 32 px x 64 co
+    case L_DCONV7:  // 64->64 transposed k5 s2: per-phase weight-stationary groups, or 8x16 coarse tiles
+      if (use_ws()) return launch_ws<64, 64, 8, 8, false, true>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 5, 2, true, 8, 16, 1, 4, NIC_NPW, 64, false, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     default:
