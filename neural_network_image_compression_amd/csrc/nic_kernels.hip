@@ -1035,7 +1035,7 @@ struct HaloPieces {
       const int row = q / RPS, r = q - row * RPS;
       const int sp = r / PSS, k = r - sp * PSS;
       const int hx = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
-      const bool read = q < TOTAL && sp < G::HW && k < PSS - 1;
+      const bool read = q < TOTAL && sp < G::HW && k < 2 * HS;  // data slots; the rest is pad
       const int slot = k < HS ? k : CIN / 8 + (k - HS);  // + c*HS per stage
       code[i] = read ? (row | hx << 8 | slot << 16 | 1 << 24) : 0;
     }
@@ -1314,13 +1314,36 @@ __global__ __launch_bounds__(64 * (NCW + NPW)) void conv_pipe_kernel(ConvArgs a)
 // (2y + py, 2x + px) for coarse position (y, x), from halo taps (iy, ix) < (KH, KW) at
 // origin (y - 1, x - 1) with weight tap tb + iy * KW + ix (host phase-major repack).
 // ------------------------------------------------------------------------------------
+// LDS halo image of the weight-stationary kernels (3x3 window, stride 1).  The B fragment
+// of v_mfma_f32_16x16x32_f16 has lane (g, l16) read channels 8g..8g+7 of pixel l16 = two
+// 8-pixel rows; a ds_read_b128 16-lane group then mixes (row 0, cols 0-3 | 4-7) and (row 1,
+// cols 4-7 | 0-3) of two channel chunks g, g+1.  Pixel records of 20 slots (64 B pad; 4 mod
+// 16) put columns 0..3 on slots 0, 4, 8, 12 (+ g), and a row pitch of 2 mod 4 slots moves
+// row 1 to the other two residues: all 16 lanes of a group hit distinct slots.
+template <int CIN, int TH, int TW>
+struct GeomWS {
+  static constexpr int HH = TH + 2, HW = TW + 2;
+  static constexpr bool S2 = false;
+  static constexpr int HE = HW;
+  static constexpr int PSB = CIN * 4 + 64;
+  static_assert((PSB / 16) % 16 == 4, "pixel record = 4 mod 16 slots");
+  static constexpr int rps() {
+    int r = HW * (PSB / 16);
+    while (r % 4 != 2) ++r;
+    return r;
+  }
+  static constexpr int RPB = rps() * 16;
+  static constexpr int HALO_BYTES = (HH * RPB + 1023) / 1024 * 1024;
+  static __device__ __forceinline__ int pix_off(int hy, int hx) { return hy * RPB + hx * PSB; }
+};
+
 template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP>
 __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
                                         int px) {
   constexpr int NTAPS = KH * KW, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
   static_assert(TW == 8 && CIN % 32 == 0 && COUT % 16 == 0, "16-pixel tiles = two 8-pixel rows");
   static_assert(!(TRP && RESID), "no residual on the transposed phases");
-  using G = GeomX3<CIN, COUT, 3, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
+  using G = GeomWS<CIN, TH, TW>;
   using HP = HaloPieces<G, CIN, CIN, NW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
 
@@ -1452,7 +1475,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 // (the phase of a transposed layer).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
 __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
-  using G = GeomX3<CIN, COUT, 3, 1, false, TH, TW, 1, 1, 1, TH * TW / 32>;
+  using G = GeomWS<CIN, TH, TW>;
   __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;

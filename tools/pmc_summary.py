@@ -21,6 +21,8 @@ LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first ma
     (r"conv1_colour", "conv1"), (r"dconv8_colour", "dconv8"), (r"dconv8_x3", "dconv8"),
     (r"<32, 64, 5, 2, false", "conv2"), (r"<64, 32, 5, 2, false", "conv8"),
     (r"<32, 64, 5, 2, true", "dconv1"), (r"<64, 64, 5, 2, true", "dconv7"),
+    (r"conv_ws_kernel<64, 64, 8, 8, false, true>", "dconv7"),
+    (r"conv_ws_kernel<64, 64, 8, 8, true, false>", "k3_resid"), (r"conv_ws_kernel<64, 64, 8, 8, false, false>", "k3"),
     (r"<64, 64, 3, 1, false.*true>", "k3_resid"), (r"<64, 64, 3, 1, false.*false>", "k3"),
     (r"latent_hist", "hist"), (r"hist_entropy", "entropy"),
 ]
