@@ -63,6 +63,7 @@ struct Dconv8Args {
   float wscale[2];      // f16x3 path: 2^-k per model
   const float* bias;    // [2]
   int nimg, H, W, tiles_x;
+  int strips, nseg, seg_rows;  // strip-walk kernel: column strips, row segments
 };
 
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);

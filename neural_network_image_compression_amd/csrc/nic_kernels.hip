@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "nic_kernels.h"
 
 namespace nic {
@@ -1887,6 +1889,186 @@ __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
 }
 
 // ------------------------------------------------------------------------------------
+// dconv8 as a strip walk (split-f16 MFMA, same A fragments and D layout as dconv8_x3).
+// A block owns a 16-wide strip of coarse columns of one image (all three planes) over a
+// segment of rows, and walks it top to bottom: every input row is fetched from HBM once
+// (plus a 2-column halo), into an R-row LDS ring, by one loader wave (LDS-DMA, R-3 rows in
+// flight), while three MFMA waves -- one per plane, weights resident -- compute output
+// row y from ring rows y-1..y+1.  Their clipped phase values meet in LDS and the Y wave
+// runs the inverse colour transform + quantiser of row y-1 before its row-y MFMAs.
+// LDS row slot: [plane][18 px][16 slots of 16 B] = the HBM pixel record [hi 64 | lo 64]
+// with slot s stored at s ^ (px & 15): the B-fragment reads (lane (g, l16) = pixel l16,
+// slot 4c + g [+ 8]) then hit 16 distinct slots per ds_read_b128 group, with no padding.
+// ------------------------------------------------------------------------------------
+#ifndef NIC_D8S_W
+#define NIC_D8S_W 16
+#endif
+#ifndef NIC_D8S_R
+#define NIC_D8S_R 5
+#endif
+constexpr int D8S_W = NIC_D8S_W;                          // coarse columns per strip
+constexpr int D8S_PX = D8S_W + 2;                         // with the halo columns
+constexpr int D8S_ROW = 3 * D8S_PX * 256;                 // 13,824 B of data per ring row
+constexpr int D8S_PIECES = (D8S_ROW + 1023) / 1024;       // 14 DMA wave-instructions per row
+constexpr int D8S_SLOT = D8S_PIECES * 1024;               // ring row stride
+constexpr int D8S_R = NIC_D8S_R;                          // ring rows
+constexpr int D8S_EX = 2 * 3 * D8S_W * 16;                // phase exchange, double-buffered
+constexpr int D8S_VMC = (D8S_R - 4) * D8S_PIECES;         // DMA pieces younger than row y+2
+static_assert(D8S_R >= 5 && D8S_VMC <= 63, "ring depth vs the 6-bit vmcnt");
+
+__global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
+  static_assert(D8S_W == 16 || D8S_W == 8, "16-lane B fragment covers one strip row (W 8: lanes 8..15 idle)");
+  __shared__ __attribute__((aligned(16))) char lds[D8S_R * D8S_SLOT + D8S_EX];
+  f32x4* ex = (f32x4*)(lds + D8S_R * D8S_SLOT);  // [row parity][plane][16 px] x 4 phases
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  int b = blockIdx.x;
+  const int seg = b % a.nseg;
+  b /= a.nseg;
+  const int strip = b % a.strips, n = b / a.strips;
+  const int x0 = strip * D8S_W;
+  const int r0 = seg * a.seg_rows, r1 = min(a.H, r0 + a.seg_rows);
+  const size_t plane_bytes = (size_t)a.H * a.W * 256;
+
+  if (wave == 3) {
+    // ---- loader wave: LDS-DMA only, so its vmcnt counts DMA pieces exactly ----
+    // per piece k: this lane's LDS slot q = 64k + lane -> (plane, px, stored slot s');
+    // source = HBM slot s' ^ (px & 15) of pixel (row, x0 - 1 + px) of that plane
+    long long src[D8S_PIECES];
+#pragma unroll
+    for (int k = 0; k < D8S_PIECES; ++k) {
+      const int q = 64 * k + lane;
+      const int pl = q / (D8S_PX * 16), r = q - pl * (D8S_PX * 16);
+      const int px = r >> 4, s = (r & 15) ^ (px & 15);
+      const int gx = x0 - 1 + px;
+      src[k] = (q < 3 * D8S_PX * 16 && gx >= 0 && gx < a.W)
+                   ? (long long)(pl * a.nimg + n) * plane_bytes + (long long)gx * 256 + s * 16
+                   : -1;
+    }
+    auto issue_row = [&](int row) {
+      char* dst = lds + ((row + D8S_R) % D8S_R) * D8S_SLOT;
+      const bool rin = row >= 0 && row < a.H;
+      const long long roff = (long long)row * a.W * 256;
+#pragma unroll
+      for (int k = 0; k < D8S_PIECES; ++k) {
+        const char* s = (rin && src[k] >= 0) ? (const char*)a.in_s + roff + src[k] : a.zero16;
+        dma16(s, dst + k * 1024);
+      }
+    };
+    // prologue: rows r0-1 .. r0+1 landed, r0+2 .. r0+R-3 in flight
+    issue_row(r0 - 1);
+    issue_row(r0);
+    issue_row(r0 + 1);
+    dma_wait_all();
+#pragma unroll
+    for (int k = 2; k <= D8S_R - 3; ++k) issue_row(r0 + k);
+    for (int y = r0; y < r1; ++y) {
+      stage_barrier();  // B_y: rows y-1..y+1 complete; row y-2's slot is free
+      issue_row(y + D8S_R - 2);
+      // row y+2 landed: all but the youngest rows y+3 .. y+R-2 are done
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (D8S_VMC & 15) | ((D8S_VMC >> 4) << 14));
+    }
+    stage_barrier();  // B_r1
+    dma_wait_all();
+    return;
+  }
+
+  // ---- MFMA wave: plane `wave` (0 Y, 1 Cb, 2 Cr) ----
+  const int model = wave > 0 ? 1 : 0;
+  f16x8 A[9][2][2];
+  {
+    const f16x8* wa = (const f16x8*)a.wx + (size_t)model * 9 * 2 * 2 * 64 + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) A[d][c][hl] = wa[((d * 2 + c) * 2 + hl) * 64];
+  }
+  const float scale = a.wscale[model], bias = a.bias[model];
+  // B-fragment offsets inside a ring row: plane `wave`, pixel l16 + dx, slot (8hl + 4c + g)
+  int boff[3][2][2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        const int px = min(l16, D8S_W - 1) + dx;  // (W 8: lanes 8..15 duplicate pixel 7, unused)
+        boff[dx][c][hl] = (wave * D8S_PX + px) * 256 + (((8 * hl + 4 * c + g) ^ (px & 15)) * 16);
+      }
+  for (int y = r0; y <= r1; ++y) {
+    stage_barrier();  // B_y
+    if (wave == 0 && y > r0 && lane < 32 && l16 < D8S_W) {  // colour epilogue of row y-1: lane = (py, px)
+      const int ry = y - 1, px = l16, py = g;
+      const int mx = x0 + px;
+      const f32x4* e = ex + ((ry & 1) * 3) * D8S_W;
+      const f32x4 yv = e[px], cbv = e[D8S_W + px], crv = e[2 * D8S_W + px];
+      if (mx < a.W) {
+        uint8_t rgb[6];
+        float rgbf[6];
+#pragma unroll
+        for (int phx = 0; phx < 2; ++phx) {
+          const int ph = py * 2 + phx;
+          const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
+          const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
+          const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) {
+            const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
+            rgbf[phx * 3 + ch] = v;
+            rgb[phx * 3 + ch] = quant255(v);
+          }
+        }
+        const int OW = a.W * 2;
+        const size_t o = (((size_t)n * a.H * 2 + 2 * ry + py) * OW + 2 * mx) * 3;
+        uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
+        d16[0] = rgb[0] | (rgb[1] << 8);
+        d16[1] = rgb[2] | (rgb[3] << 8);
+        d16[2] = rgb[4] | (rgb[5] << 8);
+        if (a.out_f32) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
+        }
+      }
+    }
+    if (y == r1) break;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // 18 groups (dy, c, dx), B fragments read three groups ahead of their MFMAs
+    const char* rows[3];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) rows[dy] = lds + ((y - 1 + dy + D8S_R) % D8S_R) * D8S_SLOT;
+    constexpr int NG = 18, DEPTH = 3;
+    f16x8 fb[DEPTH][2];
+    auto rd = [&](int gi, f16x8(&f)[2]) {
+      const int dy = gi / 6, c = (gi / 3) & 1, dx = gi % 3;
+      f[0] = *(const f16x8*)(rows[dy] + boff[dx][c][0]);
+      f[1] = *(const f16x8*)(rows[dy] + boff[dx][c][1]);
+    };
+#pragma unroll
+    for (int gi = 0; gi < DEPTH; ++gi) rd(gi, fb[gi]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      const int dy = gi / 6, c = (gi / 3) & 1, dx = gi % 3, d = dy * 3 + dx;
+      f16x8(&cur)[2] = fb[gi % DEPTH];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][1], cur[0], acc, 0, 0, 0);  // w_lo*a_hi
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], cur[1], acc, 0, 0, 0);  // w_hi*a_lo
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], cur[0], acc, 0, 0, 0);  // w_hi*a_hi
+      if (gi + DEPTH < NG) rd(gi + DEPTH, cur);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads DEPTH groups ahead
+    }
+    if (lane < D8S_W) {  // D rows 0..3 (the phases) of pixel l16
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(__fadd_rn(__fmul_rn(acc[r], scale), bias)));
+      ex[((y & 1) * 3 + wave) * D8S_W + l16] = v;
+    }
+    lds_reads_done();
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Histogram entropy (tf1_13/src/training.py:66-71) and bitstream pack/unpack
 // (utils.py:35-40).
 // ------------------------------------------------------------------------------------
@@ -2158,7 +2340,29 @@ hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// NIC_D8=tile selects the one-tile-per-block dconv8 (A/B)
+static bool use_d8_strip() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_D8");
+    return !(e && e[0] == 't');
+  }();
+  return on;
+}
+
 hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {
+  if (use_d8_strip()) {
+    a.strips = (a.W + D8S_W - 1) / D8S_W;
+    const long long units = (long long)a.nimg * a.strips;
+    // enough row segments for ~2 blocks per CU, each at least 16 rows long
+    int nseg = (int)((2LL * device_cus() + units - 1) / units);
+    nseg = std::max(1, std::min(nseg, a.H / 16));
+    a.seg_rows = (a.H + nseg - 1) / nseg;
+    a.nseg = (a.H + a.seg_rows - 1) / a.seg_rows;
+    const long long grid = units * a.nseg;
+    if (grid > INT32_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dconv8_strip_kernel, dim3((unsigned)grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
   a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
   hipLaunchKernelGGL(dconv8_x3_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
