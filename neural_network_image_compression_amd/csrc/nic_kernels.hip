@@ -1316,6 +1316,36 @@ __global__ __launch_bounds__(64 * (NCW + NPW)) void conv_pipe_kernel(ConvArgs a)
 // (2y + py, 2x + px) for coarse position (y, x), from halo taps (iy, ix) < (KH, KW) at
 // origin (y - 1, x - 1) with weight tap tb + iy * KW + ix (host phase-major repack).
 // ------------------------------------------------------------------------------------
+// 16x16 D layout -> 16-B split stores.  Lane (g, l16) holds hi and lo of 4 channels
+// (4g..4g+3 of its wave's 16); v_permlane16_swap (odd 16-lane rows of the first operand <->
+// even rows of the second) leaves even-g lanes with the hi of 8 channels [own | g+1's] and
+// odd-g lanes with the lo of the same 8 [g-1's | own]: one dwordx4 store per lane instead
+// of two dwordx2.  The swap is its own inverse (unswap16 restores a residual read in the
+// store layout to this lane's hi / lo).  Every lane must take part (EXEC full).
+__device__ __forceinline__ u32x4 swap16_pair(const f16x4& hi, const f16x4& lo) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 x = __builtin_bit_cast(u32x2, hi), y = __builtin_bit_cast(u32x2, lo);
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+    x[d] = r[0];
+    y[d] = r[1];
+  }
+  return (u32x4){x[0], x[1], y[0], y[1]};
+}
+__device__ __forceinline__ void unswap16(const u32x4& q, f16x4& hi, f16x4& lo) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 x = {q[0], q[1]}, y = {q[2], q[3]};
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+    x[d] = r[0];
+    y[d] = r[1];
+  }
+  hi = __builtin_bit_cast(f16x4, x);
+  lo = __builtin_bit_cast(f16x4, y);
+}
+
 // LDS halo image of the weight-stationary kernels (3x3 window, stride 1).  The B fragment
 // of v_mfma_f32_16x16x32_f16 has lane (g, l16) read channels 8g..8g+7 of pixel l16 = two
 // 8-pixel rows; a ds_read_b128 16-lane group then mixes (row 0, cols 0-3 | 4-7) and (row 1,
@@ -1398,30 +1428,48 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   };
 
   f32x4 acc[MT];
-  f16x4 rhi[MT], rlo[MT];  // split residual of the tile in flight (RESID)
+  u32x4 rq[MT];  // split residual of the tile in flight (RESID), in the 16-B store layout
+  // 16-B output granule of this lane after swap16_pair: [hi | lo] half (g & 1), channels
+  // 16w + 8 (g >> 1) .. +7
+  const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
   int ep_p = 0, ep_y = 0, ep_x = 0;  // tile whose epilogue is pending
+#ifdef NIC_STAMPS
+  unsigned long long s_wait = 0, s_epi = 0, s_mfma = 0, s_t0, s_t1, s_t2;
+  const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
+  NIC_PNOW(s_t2);
+#endif
   if (ntile > 0) issue(0);
   for (int i = 0; i <= ntile; ++i) {
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t0);
+    if (i > 0) s_mfma += s_t0 - s_t2;
+#endif
     dma_wait_all();  // this wave's DMAs of tile i (and the residual loads of tile i-1)
     lds_reads_done();
     stage_barrier();  // tile i's halo complete; everyone is done reading tile i-1's buffer
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t1);
+    s_wait += s_t1 - s_t0;
+#endif
     if (i > 0) {  // epilogue of tile i-1: *2^-k, bias, leaky (+ residual), split, 8-B stores
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
         f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
-          if constexpr (RESID) v[r] = __fadd_rn(v[r], __fadd_rn((float)rhi[m][r], (float)rlo[m][r]));
+        for (int r = 0; r < 4; ++r) v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
+        if constexpr (RESID) {
+          f16x4 rh, rl;
+          unswap16(rq[m], rh, rl);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = __fadd_rn(v[r], __fadd_rn((float)rh[r], (float)rl[r]));
         }
         f16x4 hi, lo;
         split4(v, hi, lo);
+        u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
         if (y < a.H && x < a.W) {
           const int oy = TRP ? 2 * y + py : y, ox = TRP ? 2 * x + px : x;
-          uint16_t* o = a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + co0;
-          *(f16x4*)o = hi;
-          *(f16x4*)(o + COUT) = lo;
+          *(u32x4*)(a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = q;
         }
       }
     }
@@ -1432,12 +1480,14 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int oy = min(ep_y + 2 * m + (l16 >> 3), a.OH - 1), ox = min(ep_x + (l16 & 7), a.OW - 1);
-        const uint16_t* r = a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + co0;
-        rhi[m] = *(const f16x4*)r;
-        rlo[m] = *(const f16x4*)(r + COUT);
+        rq[m] = *(const u32x4*)(a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off);
       }
     }
     const char* buf = lds + (i & 1) * G::HALO_BYTES;
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t2);
+    s_epi += s_t2 - s_t1;
+#endif
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // NTAPS x KST k32-steps, fully unrolled (the weight registers are indexed statically).
@@ -1471,6 +1521,19 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
       }
     }
   }
+#ifdef NIC_STAMPS
+  if (threadIdx.x == 0) {
+    unsigned long long* o = g_stamps + blockIdx.x * 8;
+    o[0] = s_wait;
+    o[1] = s_epi;
+    o[2] = s_mfma;
+    o[3] = ntile;
+    o[4] = __builtin_amdgcn_s_memtime() - s_c0;
+    o[5] = __builtin_amdgcn_s_memrealtime() - s_rt0;
+    o[6] = NTAPS;
+    o[7] = model;
+  }
+#endif
 }
 
 // Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi & 1, tap set gi >> 1
