@@ -28,12 +28,25 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <utility>
 
 #include "nic_kernels.h"
 
 namespace nic {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1 (register arrays
+// indexed by I stay registers however large the body; #pragma unroll may give up).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __constant__ float c_u8_to_unit[256];  // fp32(i) / 255, correctly rounded (host-computed)
@@ -1536,6 +1549,199 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #endif
 }
 
+// ------------------------------------------------------------------------------------
+// Weight-stationary persistent conv for the k5 s2 forward layers (conv2 32->64, conv8
+// 64->32 -> u8 latent), split-f16 on v_mfma_f32_16x16x32_f16.  25 taps of resident
+// weights do not fit one wave's registers, so a block of 8 waves (two per SIMD, one block
+// per CU) splits them: wave w = (cg = w % NCG: output channels 16cg..16cg+15, ts = w / NCG:
+// taps [25 ts / NTS, 25 (ts+1) / NTS)).  Waves ts > 0 leave their partial sums of a tile
+// in LDS (double-buffered by tile parity); the ts = 0 waves add them in the deferred
+// epilogue at the start of the next tile, while the others already run its MFMAs.
+// Halo: (2 TH + 3) x (2 TW + 3) input pixels, columns stored even-first then odd (so the
+// 8 output columns of a 16-pixel B fragment read consecutive records), records of
+// Cin / 4 + 2 slots and a row pitch of 0 mod 8 slots: conflict-free ds_read_b128.
+// ------------------------------------------------------------------------------------
+template <int CIN, int TH, int TW>
+struct GeomS2 {
+  static constexpr int HH = (TH - 1) * 2 + 5, HW = (TW - 1) * 2 + 5, HE = (HW + 1) / 2;
+  static constexpr int PSS = CIN / 4 + 2, PSB = PSS * 16;  // data slots + 2 pad
+  static constexpr int RPS = (HW * PSS + 7) / 8 * 8, RPB = RPS * 16;
+  static constexpr int HTOT = HH * RPS;  // slots
+  static constexpr int NPIECE = (HTOT + 63) / 64;
+  static constexpr int HALO_BYTES = NPIECE * 1024;
+  static __device__ __forceinline__ int col(int hx) { return (hx & 1) * HE + (hx >> 1); }
+};
+
+template <int CIN, int COUT, int NTS, int OUT_MODE, int TS>
+__device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
+  constexpr int TH = 8, TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
+  constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
+  using G = GeomS2<CIN, TH, TW>;
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+  constexpr int NPP = (G::NPIECE + NW - 1) / NW;
+  constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
+  char* part = lds + 2 * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave % NCG;
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int per_plane = a.tiles_y * a.tiles_x;
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  const int ntot = np * per_plane;
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+
+  f16x8 wr[NT][KST][2];
+  {
+    const char* wsrc = (const char*)a.wx + ((size_t)model * 25 + T0) * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          wr[t][ks][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
+                                          ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
+  }
+  const float scale = a.wscale[model];
+  const int co0 = cg * 16 + 4 * g;
+  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
+  // B fragment of pixel tile m: output pixel (2m + l16/8, l16%8) -> halo row 2 (2m + l16/8),
+  // stored column l16%8 (tap (0,0)); channels 8g..8g+7
+  int boff[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
+  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
+    const int t = bi + i * nb;
+    const int pl = t / per_plane;
+    p = p0 + pl;
+    const int r = t - pl * per_plane, ty = r / a.tiles_x;
+    t0y = ty * TH;
+    t0x = (r - ty * a.tiles_x) * TW;
+  };
+  // this wave's DMA pieces of a halo: slot q -> (row, stored pixel sp, slot k)
+  auto issue = [&](int i) {
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    const int gy0 = 2 * t0y - a.pad_y, gx0 = 2 * t0x - a.pad_x;
+    const char* base = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
+    char* buf = lds + (i & 1) * G::HALO_BYTES;
+#pragma unroll
+    for (int j = 0; j < NPP; ++j) {
+      const int piece = wave + j * NW;
+      if (NPP * NW > G::NPIECE && piece >= G::NPIECE) break;  // wave-uniform
+      const int q = piece * 64 + lane;
+      const int row = q / G::RPS, r = q - row * G::RPS;
+      const int sp = r / G::PSS, k = r - sp * G::PSS;
+      const int hx = sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1;
+      const int gy = gy0 + row, gx = gx0 + hx;
+      const bool ok = q < G::HTOT && sp < G::HW && k < CIN / 4 && (unsigned)gy < (unsigned)a.H &&
+                      (unsigned)gx < (unsigned)a.W;
+      dma16(ok ? base + ((size_t)(unsigned)(gy * a.W + gx) * CIN * 4 + k * 16) : a.zero16, buf + piece * 1024);
+    }
+  };
+
+  f32x4 acc[MT];
+  const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
+  int ep_p = 0, ep_y = 0, ep_x = 0;
+  if (ntile > 0) issue(0);
+  for (int i = 0; i <= ntile; ++i) {
+    dma_wait_all();
+    lds_reads_done();
+    stage_barrier();  // halo of tile i complete; partials of tile i-1 written
+    if constexpr (TS == 0) {
+      if (i > 0) {  // epilogue of tile i-1: own sums + the other tap groups' partials
+        const char* pp = part + (((i - 1) & 1) * (NTS - 1) * NCG + cg) * PART + lane * 16;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+#pragma unroll
+          for (int s = 1; s < NTS; ++s) {
+            const f32x4 q = *(const f32x4*)(pp + ((s - 1) * NCG) * PART + m * 1024);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
+          }
+          const int oy = ep_y + 2 * m + (l16 >> 3), ox = ep_x + (l16 & 7);
+          f32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
+          if constexpr (OUT_MODE == OUT_SPLIT) {
+            f16x4 hi, lo;
+            split4(v, hi, lo);
+            const u32x4 q = swap16_pair(hi, lo);
+            if (oy < a.OH && ox < a.OW)
+              *(u32x4*)(a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = q;
+          } else {  // clip, round(x*255) into the latent layout (N, h, w, 96)
+            if (oy < a.OH && ox < a.OW) {
+              const int n = ep_p % a.nimg, type = ep_p / a.nimg;
+              const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co0;
+              uint32_t packed = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                v[r] = clip01(v[r]);
+                packed |= (uint32_t)quant255(v[r]) << (8 * r);
+              }
+              *(uint32_t*)(a.out_u8 + lo) = packed;
+              if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
+            }
+          }
+        }
+      }
+    }
+    if (i == ntile) break;
+    if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
+    tile_at(i, ep_p, ep_y, ep_x);
+    const char* buf = lds + (i & 1) * G::HALO_BYTES;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // NT taps x KST k32-steps x MT pixel tiles, B fragments read DEPTH groups ahead
+    constexpr int NG = NT * KST * MT, DEPTH = 3;
+    auto grp_off = [&](int gq) {
+      const int st = gq / MT, m = gq - st * MT;
+      const int t = T0 + st / KST, ks = st % KST, kh = t / 5, kw = t - kh * 5;
+      return boff[m] + kh * G::RPB + G::col(kw) * G::PSB + ks * 64;
+    };
+    f16x8 fb[DEPTH][2];
+#pragma unroll
+    for (int gq = 0; gq < DEPTH; ++gq) {
+      fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
+      fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
+    }
+    static_for<NG>([&](auto gqc) {
+      constexpr int gq = decltype(gqc)::value;
+      constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;
+      f16x8(&cur)[2] = fb[gq % DEPTH];
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], acc[m], 0, 0, 0);  // w_lo*a_hi
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], acc[m], 0, 0, 0);  // w_hi*a_lo
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], acc[m], 0, 0, 0);  // w_hi*a_hi
+      if constexpr (gq + DEPTH < NG) {
+        cur[0] = *(const f16x8*)(buf + grp_off(gq + DEPTH));
+        cur[1] = *(const f16x8*)(buf + grp_off(gq + DEPTH) + CIN * 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the stream order
+    });
+    if constexpr (TS > 0) {  // partial sums of tile i for the ts = 0 wave of this cg
+      char* pp = part + (((i & 1) * (NTS - 1) + TS - 1) * NCG + cg) * PART + lane * 16;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+    }
+  }
+}
+
+template <int CIN, int COUT, int NTS, int OUT_MODE>
+__global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
+  using G = GeomS2<CIN, 8, 8>;
+  constexpr int NCG = COUT / 16;
+  static_assert(NCG * NTS == 8, "8 waves per block");
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 2 * (NTS - 1) * NCG * 4 * 1024];
+  int gi = 0;
+  while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
+  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
+  static_for<NTS>([&](auto tsc) {
+    constexpr int TS = decltype(tsc)::value;
+    if (ts == TS) ws2_wave<CIN, COUT, NTS, OUT_MODE, TS>(a, lds, gi, bi, nb);
+  });
+}
+
 // Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi & 1, tap set gi >> 1
 // (the phase of a transposed layer).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
@@ -2355,9 +2561,35 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
+// proportion to their planes.
+template <int CIN, int COUT, int NTS, int OUT_MODE>
+static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
+  a.tiles_y = (a.OH + 7) / 8;
+  a.tiles_x = (a.OW + 7) / 8;
+  const long long per_plane = (long long)a.tiles_y * a.tiles_x;
+  const long long nt = per_plane * a.P;
+  if (nt == 0) return hipSuccess;
+  if (nt > INT32_MAX || a.P != 3 * a.nimg) return hipErrorInvalidValue;
+  a.ntiles = (int)nt;
+  a.ws_taps = 25;
+  a.ws_ngrp = 2;
+  const int target = device_cus();
+  const long long ty = per_plane * a.nimg, tc = per_plane * (a.P - a.nimg);
+  long long by = (target + 1) / 3;
+  by = std::max(1LL, std::min(by, ty));
+  long long bc = std::max(1LL, std::min((long long)target - by, tc));
+  a.ws_blk[0] = 0;
+  a.ws_blk[1] = (int)by;
+  a.ws_blk[2] = (int)(by + bc);
+  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
-    case L_CONV2:  // 32->64 k5 s2: 8x8 tile, 2 waves split N, each 64 px x 32 co
+    case L_CONV2:  // 32->64 k5 s2: tap-split weight-stationary, or 8x8 tile, 2 waves split N
+      if (use_ws()) return launch_ws2<32, 64, 2, OUT_SPLIT>(a, st);
       return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
                    // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
