@@ -34,6 +34,8 @@
 
 namespace nic {
 
+static int device_cus();  // CUs of the current device (cached)
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1 (register arrays
 // indexed by I stay registers however large the body; #pragma unroll may give up).
@@ -1367,11 +1369,11 @@ __device__ __forceinline__ void unswap16(const u32x4& q, f16x4& hi, f16x4& lo) {
 // row 1 to the other two residues: all 16 lanes of a group hit distinct slots.
 template <int CIN, int TH, int TW>
 struct GeomWS {
+  static_assert(CIN == 64, "record geometry searched for Cin 64");
   static constexpr int HH = TH + 2, HW = TW + 2;
   static constexpr bool S2 = false;
   static constexpr int HE = HW;
   static constexpr int PSB = CIN * 4 + 64;
-  static_assert((PSB / 16) % 16 == 4, "pixel record = 4 mod 16 slots");
   static constexpr int rps() {
     int r = HW * (PSB / 16);
     while (r % 4 != 2) ++r;
@@ -1572,9 +1574,9 @@ struct GeomS2 {
   static __device__ __forceinline__ int col(int hx) { return (hx & 1) * HE + (hx >> 1); }
 };
 
-template <int CIN, int COUT, int NTS, int OUT_MODE, int TS>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
-  constexpr int TH = 8, TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
+  constexpr int TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
@@ -1726,19 +1728,19 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   }
 }
 
-template <int CIN, int COUT, int NTS, int OUT_MODE>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE>
 __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
-  using G = GeomS2<CIN, 8, 8>;
+  using G = GeomS2<CIN, TH, 8>;
   constexpr int NCG = COUT / 16;
   static_assert(NCG * NTS == 8, "8 waves per block");
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 2 * (NTS - 1) * NCG * 4 * 1024];
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 2 * (NTS - 1) * NCG * (TH / 2) * 1024];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
-    if (ts == TS) ws2_wave<CIN, COUT, NTS, OUT_MODE, TS>(a, lds, gi, bi, nb);
+    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS>(a, lds, gi, bi, nb);
   });
 }
 
@@ -2563,9 +2565,9 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
 
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
 // proportion to their planes.
-template <int CIN, int COUT, int NTS, int OUT_MODE>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE>
 static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
-  a.tiles_y = (a.OH + 7) / 8;
+  a.tiles_y = (a.OH + TH - 1) / TH;
   a.tiles_x = (a.OW + 7) / 8;
   const long long per_plane = (long long)a.tiles_y * a.tiles_x;
   const long long nt = per_plane * a.P;
@@ -2582,14 +2584,14 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = (int)by;
   a.ws_blk[2] = (int)(by + bc);
-  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
     case L_CONV2:  // 32->64 k5 s2: tap-split weight-stationary, or 8x8 tile, 2 waves split N
-      if (use_ws()) return launch_ws2<32, 64, 2, OUT_SPLIT>(a, st);
+      if (use_ws()) return launch_ws2<32, 64, 2, 8, OUT_SPLIT>(a, st);
       return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
                    // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
@@ -2600,7 +2602,9 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
       if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
       if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
-    case L_CONV8:  // 64->32 k5 s2 -> latent: 4x8 tile, taps split over 4 waves
+    case L_CONV8:  // 64->32 k5 s2 -> latent: tap-split weight-stationary (2 channel groups x 4 tap
+                   // quarters, 4x8 tiles), or 4x8 tile with taps split over 4 waves
+      if (use_ws()) return launch_ws2<64, 32, 4, 4, OUT_U8_LATENT>(a, st);
       return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_SPLIT, OUT_U8_LATENT, false>(a, st);
     case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
       return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
