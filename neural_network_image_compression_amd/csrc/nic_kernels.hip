@@ -2163,21 +2163,18 @@ __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
 // dconv8 as a strip walk (split-f16 MFMA, same A fragments and D layout as dconv8_x3).
 // A block owns a 16-wide strip of coarse columns of one image (all three planes) over a
 // segment of rows, and walks it top to bottom: every input row is fetched from HBM once
-// (plus a 2-column halo), into an R-row LDS ring, by one loader wave (LDS-DMA, R-3 rows in
-// flight), while three MFMA waves -- one per plane, weights resident -- compute output
-// row y from ring rows y-1..y+1.  Their clipped phase values meet in LDS and the Y wave
-// runs the inverse colour transform + quantiser of row y-1 before its row-y MFMAs.
+// (plus a 2-column halo), into an R-row LDS ring by LDS-DMA (every wave issues a quarter of
+// each row's pieces; R-3 rows in flight), while three MFMA waves -- one per plane, weights
+// resident -- compute output row y from ring rows y-1..y+1.  Their clipped phase values
+// meet in LDS and the fourth wave runs the inverse colour transform + quantiser of row y-1.
 // LDS row slot: [plane][18 px][16 slots of 16 B] = the HBM pixel record [hi 64 | lo 64]
 // with slot s stored at s ^ (px & 15): the B-fragment reads (lane (g, l16) = pixel l16,
 // slot 4c + g [+ 8]) then hit 16 distinct slots per ds_read_b128 group, with no padding.
 // ------------------------------------------------------------------------------------
-#ifndef NIC_D8S_W
-#define NIC_D8S_W 16
-#endif
 #ifndef NIC_D8S_R
 #define NIC_D8S_R 5
 #endif
-constexpr int D8S_W = NIC_D8S_W;                          // coarse columns per strip
+constexpr int D8S_W = 16;                                 // coarse columns per strip
 constexpr int D8S_PX = D8S_W + 2;                         // with the halo columns
 constexpr int D8S_ROW = 3 * D8S_PX * 256;                 // 13,824 B of data per ring row
 constexpr int D8S_PIECES = (D8S_ROW + 1023) / 1024;       // 14 DMA wave-instructions per row
@@ -2188,7 +2185,6 @@ constexpr int D8S_VMC = (D8S_R - 4) * D8S_PIECES;         // DMA pieces younger 
 static_assert(D8S_R >= 5 && D8S_VMC <= 63, "ring depth vs the 6-bit vmcnt");
 
 __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
-  static_assert(D8S_W == 16 || D8S_W == 8, "16-lane B fragment covers one strip row (W 8: lanes 8..15 idle)");
   __shared__ __attribute__((aligned(16))) char lds[D8S_R * D8S_SLOT + D8S_EX];
   f32x4* ex = (f32x4*)(lds + D8S_R * D8S_SLOT);  // [row parity][plane][16 px] x 4 phases
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2201,46 +2197,90 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
   const int r0 = seg * a.seg_rows, r1 = min(a.H, r0 + a.seg_rows);
   const size_t plane_bytes = (size_t)a.H * a.W * 256;
 
+  // ---- loading, shared by the four waves: wave w DMAs pieces w, w+4, ... of every row ----
+  // piece k: LDS slot q = 64k + lane -> (plane, px, stored slot s'); source = HBM slot
+  // s' ^ (px & 15) of pixel (row, x0 - 1 + px) of that plane
+  constexpr int NPW = (D8S_PIECES + 3) / 4;
+  const int npw = (D8S_PIECES - wave + 3) / 4;  // this wave's pieces per row (NPW or NPW-1)
+  long long src[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int q = 64 * (wave + 4 * j) + lane;
+    const int pl = q / (D8S_PX * 16), r = q - pl * (D8S_PX * 16);
+    const int px = r >> 4, s = (r & 15) ^ (px & 15);
+    const int gx = x0 - 1 + px;
+    src[j] = (q < 3 * D8S_PX * 16 && gx >= 0 && gx < a.W)
+                 ? (long long)(pl * a.nimg + n) * plane_bytes + (long long)gx * 256 + s * 16
+                 : -1;
+  }
+  auto issue_row = [&](int row) {
+    char* dst = lds + ((row + D8S_R) % D8S_R) * D8S_SLOT;
+    const bool rin = row >= 0 && row < a.H;
+    const long long roff = (long long)row * a.W * 256;
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      if (j == NPW - 1 && npw < NPW) break;  // wave-uniform
+      const char* s = (rin && src[j] >= 0) ? (const char*)a.in_s + roff + src[j] : a.zero16;
+      dma16(s, dst + (wave + 4 * j) * 1024);
+    }
+  };
+  // row y+2 landed: all but this wave's pieces of rows y+3 .. y+R-2 are done
+  auto wait_row = [&]() {
+    if (npw == NPW)
+      __builtin_amdgcn_s_waitcnt(0x0F70 | ((NPW * (D8S_R - 4)) & 15) | (((NPW * (D8S_R - 4)) >> 4) << 14));
+    else
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (((NPW - 1) * (D8S_R - 4)) & 15) | ((((NPW - 1) * (D8S_R - 4)) >> 4) << 14));
+  };
+  // prologue: rows r0-1 .. r0+1 landed, r0+2 .. r0+R-3 in flight
+  issue_row(r0 - 1);
+  issue_row(r0);
+  issue_row(r0 + 1);
+  dma_wait_all();
+#pragma unroll
+  for (int k = 2; k <= D8S_R - 3; ++k) issue_row(r0 + k);
+
   if (wave == 3) {
-    // ---- loader wave: LDS-DMA only, so its vmcnt counts DMA pieces exactly ----
-    // per piece k: this lane's LDS slot q = 64k + lane -> (plane, px, stored slot s');
-    // source = HBM slot s' ^ (px & 15) of pixel (row, x0 - 1 + px) of that plane
-    long long src[D8S_PIECES];
+    // ---- colour epilogue wave: row y-1 from the phase exchange, stores after its vmcnt
+    // wait so that they are older than the next rows' pieces ----
+    for (int y = r0; y <= r1; ++y) {
+      stage_barrier();  // B_y: rows y-1..y+1 complete; ex[(y-1)&1] holds row y-1
+      if (y < r1) issue_row(y + D8S_R - 2);
+      const int ry = y - 1, px = l16, py = g, mx = x0 + px;
+      const bool act = y > r0 && lane < 32 && mx < a.W;
+      uint8_t rgb[6];
+      float rgbf[6];
+      if (act) {
+        const f32x4* e = ex + ((ry & 1) * 3) * D8S_W;
+        const f32x4 yv = e[px], cbv = e[D8S_W + px], crv = e[2 * D8S_W + px];
 #pragma unroll
-    for (int k = 0; k < D8S_PIECES; ++k) {
-      const int q = 64 * k + lane;
-      const int pl = q / (D8S_PX * 16), r = q - pl * (D8S_PX * 16);
-      const int px = r >> 4, s = (r & 15) ^ (px & 15);
-      const int gx = x0 - 1 + px;
-      src[k] = (q < 3 * D8S_PX * 16 && gx >= 0 && gx < a.W)
-                   ? (long long)(pl * a.nimg + n) * plane_bytes + (long long)gx * 256 + s * 16
-                   : -1;
-    }
-    auto issue_row = [&](int row) {
-      char* dst = lds + ((row + D8S_R) % D8S_R) * D8S_SLOT;
-      const bool rin = row >= 0 && row < a.H;
-      const long long roff = (long long)row * a.W * 256;
+        for (int phx = 0; phx < 2; ++phx) {
+          const int ph = py * 2 + phx;
+          const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
+          const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
+          const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
 #pragma unroll
-      for (int k = 0; k < D8S_PIECES; ++k) {
-        const char* s = (rin && src[k] >= 0) ? (const char*)a.in_s + roff + src[k] : a.zero16;
-        dma16(s, dst + k * 1024);
+          for (int ch = 0; ch < 3; ++ch) {
+            const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
+            rgbf[phx * 3 + ch] = v;
+            rgb[phx * 3 + ch] = quant255(v);
+          }
+        }
       }
-    };
-    // prologue: rows r0-1 .. r0+1 landed, r0+2 .. r0+R-3 in flight
-    issue_row(r0 - 1);
-    issue_row(r0);
-    issue_row(r0 + 1);
-    dma_wait_all();
+      lds_reads_done();
+      if (y < r1) wait_row();
+      if (act) {
+        const size_t o = (((size_t)n * a.H * 2 + 2 * ry + py) * (a.W * 2) + 2 * mx) * 3;
+        uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
+        d16[0] = rgb[0] | (rgb[1] << 8);
+        d16[1] = rgb[2] | (rgb[3] << 8);
+        d16[2] = rgb[4] | (rgb[5] << 8);
+        if (a.out_f32) {
 #pragma unroll
-    for (int k = 2; k <= D8S_R - 3; ++k) issue_row(r0 + k);
-    for (int y = r0; y < r1; ++y) {
-      stage_barrier();  // B_y: rows y-1..y+1 complete; row y-2's slot is free
-      issue_row(y + D8S_R - 2);
-      // row y+2 landed: all but the youngest rows y+3 .. y+R-2 are done
-      __builtin_amdgcn_s_waitcnt(0x0F70 | (D8S_VMC & 15) | ((D8S_VMC >> 4) << 14));
+          for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
+        }
+      }
     }
-    stage_barrier();  // B_r1
-    dma_wait_all();
+    dma_wait_all();  // no LDS-DMA outlives the wave
     return;
   }
 
@@ -2265,45 +2305,28 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) {
-        const int px = min(l16, D8S_W - 1) + dx;  // (W 8: lanes 8..15 duplicate pixel 7, unused)
+        const int px = l16 + dx;
         boff[dx][c][hl] = (wave * D8S_PX + px) * 256 + (((8 * hl + 4 * c + g) ^ (px & 15)) * 16);
       }
+#ifdef NIC_STAMPS
+  unsigned long long sb = 0, si = 0, sm = 0, sw = 0, t0, t1, t2, t3, t4;
+  NIC_PNOW(t4);
+#endif
   for (int y = r0; y <= r1; ++y) {
+#ifdef NIC_STAMPS
+    NIC_PNOW(t0);
+#endif
     stage_barrier();  // B_y
-    if (wave == 0 && y > r0 && lane < 32 && l16 < D8S_W) {  // colour epilogue of row y-1: lane = (py, px)
-      const int ry = y - 1, px = l16, py = g;
-      const int mx = x0 + px;
-      const f32x4* e = ex + ((ry & 1) * 3) * D8S_W;
-      const f32x4 yv = e[px], cbv = e[D8S_W + px], crv = e[2 * D8S_W + px];
-      if (mx < a.W) {
-        uint8_t rgb[6];
-        float rgbf[6];
-#pragma unroll
-        for (int phx = 0; phx < 2; ++phx) {
-          const int ph = py * 2 + phx;
-          const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
-          const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
-          const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {
-            const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
-            rgbf[phx * 3 + ch] = v;
-            rgb[phx * 3 + ch] = quant255(v);
-          }
-        }
-        const int OW = a.W * 2;
-        const size_t o = (((size_t)n * a.H * 2 + 2 * ry + py) * OW + 2 * mx) * 3;
-        uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
-        d16[0] = rgb[0] | (rgb[1] << 8);
-        d16[1] = rgb[2] | (rgb[3] << 8);
-        d16[2] = rgb[4] | (rgb[5] << 8);
-        if (a.out_f32) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
-        }
-      }
-    }
+#ifdef NIC_STAMPS
+    NIC_PNOW(t1);
+    sb += t1 - t0;
+#endif
     if (y == r1) break;
+    issue_row(y + D8S_R - 2);
+#ifdef NIC_STAMPS
+    NIC_PNOW(t2);
+    si += t2 - t1;
+#endif
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     // 18 groups (dy, c, dx), B fragments read three groups ahead of their MFMAs
     const char* rows[3];
@@ -2329,14 +2352,33 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
       if (gi + DEPTH < NG) rd(gi + DEPTH, cur);
       __builtin_amdgcn_sched_barrier(0);  // keep the reads DEPTH groups ahead
     }
-    if (lane < D8S_W) {  // D rows 0..3 (the phases) of pixel l16
+    if (lane < 16) {  // D rows 0..3 (the phases) of pixel l16
       f32x4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(__fadd_rn(__fmul_rn(acc[r], scale), bias)));
       ex[((y & 1) * 3 + wave) * D8S_W + l16] = v;
     }
     lds_reads_done();
+#ifdef NIC_STAMPS
+    NIC_PNOW(t3);
+    sm += t3 - t2;
+#endif
+    wait_row();
+#ifdef NIC_STAMPS
+    NIC_PNOW(t4);
+    sw += t4 - t3;
+#endif
   }
+  dma_wait_all();
+#ifdef NIC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_stamps + (blockIdx.x * 4 + wave) * 4;
+    o[0] = sb;
+    o[1] = si;
+    o[2] = sm;
+    o[3] = sw;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------
