@@ -139,7 +139,30 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
     out.assign(26 * 32, 0.f);
     for (int t = 0; t < 25; ++t)
       for (int co = 0; co < 32; ++co) out[t * 32 + co] = K[t * 32 + co];
-    return -1000;
+    // split-f16 MFMA A fragments of the fused conv1 (v_mfma_f32_16x16x32_f16, K = taps padded
+    // to 32): [co tile ct][hi,lo][lane][j], lane l holds row co = 16ct + (l & 15) and tap
+    // t = 8 (l >> 4) + j (zero for t >= 25), scaled by 2^k so every value is a normal f16 pair
+    float maxabs = 0.f;
+    for (int i = 0; i < 25 * 32; ++i) maxabs = std::max(maxabs, std::fabs(K[i]));
+    int kexp = 0;
+    if (maxabs > 0.f && std::isfinite(maxabs)) {
+      int e = 0;
+      std::frexp(maxabs, &e);
+      kexp = std::min(std::max(15 - e, -100), 100);
+    }
+    outx.assign((size_t)2 * 2 * 64 * 8, 0);
+    for (int ct = 0; ct < 2; ++ct)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int t = 8 * (lane >> 4) + j, co = 16 * ct + (lane & 15);
+          if (t >= 25) continue;
+          const float w = std::ldexp(K[t * 32 + co], kexp);
+          const _Float16 hi = (_Float16)w;
+          const _Float16 lo = (_Float16)(w - (float)hi);
+          std::memcpy(&outx[(((size_t)ct * 2 + 0) * 64 + lane) * 8 + j], &hi, 2);
+          std::memcpy(&outx[(((size_t)ct * 2 + 1) * 64 + lane) * 8 + j], &lo, 2);
+        }
+    return kexp;
   }
   if (L.id == L_DCONV8) {  // (5,5,1,64) (kh,kw,Cout,Cin) -> [25 phase taps][64]
     out.assign(25 * 64, 0.f);
@@ -407,14 +430,16 @@ int nic_create(int device, nic_ctx** out) {
     for (int i = 0; i < 5; ++i) {
       const LayerSpec& L = tab[i];
       const size_t kb = 2 * packed_kernel_floats(L) * sizeof(float), bb = 2 * L.cout * sizeof(float);
+      // split-f16 fragments: dconv8 [2][9][2][2][64][8], conv1 [2][2][2][64][8], else as wk
+      const size_t xb = L.id == L_DCONV8 ? 2 * 9 * 2 * 2 * 64 * 16 : L.id == L_CONV1 ? 2 * 2 * 2 * 64 * 16 : kb;
       if (hipMalloc(&c->wk[L.id], kb) != hipSuccess || hipMalloc(&c->wb[L.id], bb) != hipSuccess ||
-          (L.cin >= 32 && hipMalloc(&c->wx[L.id], L.id == L_DCONV8 ? 2 * 9 * 2 * 2 * 64 * 16 : kb) != hipSuccess)) {
+          hipMalloc(&c->wx[L.id], xb) != hipSuccess) {
         nic_destroy(c);
         return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
       }
       (void)hipMemset(c->wk[L.id], 0, kb);
       (void)hipMemset(c->wb[L.id], 0, bb);
-      if (c->wx[L.id]) (void)hipMemset(c->wx[L.id], 0, L.id == L_DCONV8 ? 2 * 9 * 2 * 2 * 64 * 16 : kb);
+      (void)hipMemset(c->wx[L.id], 0, xb);
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
     }
   }
@@ -561,7 +586,9 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
   a1.OW = g.c1x.out;
   a1.pad_y = g.c1y.lo;
   a1.pad_x = g.c1x.lo;
-  TIMED(L_CONV1, launch_conv1(a1, st));
+  // f16x3: conv1 runs inside the conv2 kernel (launch_conv12_x3, timed as conv2)
+  const bool fuse12 = c->precision == NIC_PRECISION_F16X3 && conv12_fused();
+  if (!fuse12) TIMED(L_CONV1, launch_conv1(a1, st));
 
   auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW, int py,
                   int px) {
@@ -589,7 +616,21 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
     return a;
   };
   const int h1 = g.c1y.out, w1 = g.c1x.out, h2 = g.c2y.out, w2 = g.c2x.out;
-  TIMED(L_CONV2, run_layer(c, L_CONV2, conv(L_CONV2, R[0], R[1], nullptr, h1, w1, h2, w2, g.c2y.lo, g.c2x.lo), st));
+  ConvArgs a2 = conv(L_CONV2, R[0], R[1], nullptr, h1, w1, h2, w2, g.c2y.lo, g.c2x.lo);
+  if (fuse12) {
+    a2.rgb = rgb;
+    a2.wx1 = c->wx[L_CONV1];
+    a2.wscale1[0] = c->wscale[L_CONV1][0];
+    a2.wscale1[1] = c->wscale[L_CONV1][1];
+    a2.bias1 = c->wb[L_CONV1];
+    a2.H0 = h;
+    a2.W0 = w;
+    a2.p1y = g.c1y.lo;
+    a2.p1x = g.c1x.lo;
+    TIMED(L_CONV2, launch_conv12_x3(a2, st));
+  } else {
+    TIMED(L_CONV2, run_layer(c, L_CONV2, a2, st));
+  }
   TIMED(L_CONV3, run_layer(c, L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1), st));
   TIMED(L_CONV4, run_layer(c, L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1), st));
   ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);

@@ -41,6 +41,14 @@ struct ConvArgs {
   int ws_taps;            // weight-stationary kernels: taps per model in wx
   int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
+  // conv1 fused into conv2 (f16x3): the colour plane is computed from the RGB input and
+  // conv1's split output is written straight into conv2's LDS halo (no HBM round trip)
+  const uint8_t* rgb;     // [N][H0][W0][3]
+  const uint16_t* wx1;    // conv1 MFMA A fragments [2 models][2 co tiles][hi,lo][64 lanes][8] of w*2^k
+  float wscale1[2];       // 2^-k per model for wx1
+  const float* bias1;     // [2][32]
+  int H0, W0;             // image size (conv1 input)
+  int p1y, p1x;           // conv1 TF-SAME pad_lo
 };
 
 struct Conv1Args {
@@ -69,6 +77,8 @@ struct Dconv8Args {
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA
+hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st);  // conv1 fused into conv2 (f16x3)
+bool conv12_fused();  // whether nic_encode uses launch_conv12_x3 in f16x3 mode
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);      // exact fp32 VALU
 hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st);   // split-f16 MFMA

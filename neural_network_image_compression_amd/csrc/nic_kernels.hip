@@ -1574,15 +1574,28 @@ struct GeomS2 {
   static __device__ __forceinline__ int col(int hx) { return (hx & 1) * HE + (hx >> 1); }
 };
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS>
+// conv1 fused into conv2 (FUSE1): per tile the 41 x 41 colour-plane patch conv1's 19 x 19
+// halo outputs need is computed from the RGB bytes (loaded into registers by the ts = 1
+// waves while the previous tile's MFMAs run), conv1 runs on the same split-f16 MFMA
+// (K = 25 taps padded to 32; B = im2col gathered from the patch, split on the fly) and its
+// bias + leaky + split outputs land directly in the conv2 halo (zero outside conv1's output,
+// conv2's SAME padding).  The halo and the patch are single LDS buffers: each tile runs
+// [epilogue(i-1) | patch(i)] -> barrier -> conv1(i) -> barrier -> conv2 MFMAs(i).
+constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
+
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
+  static_assert(!FUSE1 || (CIN == 32 && TH == 8 && G::HH == 19 && NTS == 2 && OUT_MODE == OUT_SPLIT),
+                "conv1 fusion is conv2's 8x8-tile form");
   constexpr int TAP_BYTES = CIN * COUT * 4;
   constexpr int NPP = (G::NPIECE + NW - 1) / NW;
   constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
-  char* part = lds + 2 * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
+  char* part = lds + (FUSE1 ? 1 : 2) * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
+  float* plane = (float*)(part + 2 * (NTS - 1) * NCG * PART);  // FUSE1: colour-plane patch
+  float* lut = plane + C12_PH * C12_PH;                        // FUSE1: u8 -> fp32 / 255
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -1642,10 +1655,58 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
   };
 
+  // ---- FUSE1 state: conv1 A fragments / bias / scale, this lane's im2col tap offsets in the
+  // patch (-1: pad tap >= 25), and the RGB bytes of the next patch (ts = 1 waves) ----
+  f16x8 A1[2][2];
+  f32x4 b1[2];
+  int toff[8];
+  float scale1 = 1.f;
+  constexpr int NRGB = (C12_PH * C12_PH + 255) / 256;  // patch pixels per ts = 1 thread
+  uint32_t rgbv[NRGB];  // r | g << 8 | b << 16 | inside << 24 (used by the ts = 1 waves)
+  const int tid1 = (int)threadIdx.x - 256;
+  int pl_type = 0;  // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgbv
+  auto rgb_load = [&](int i) {
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    const int n = p % a.nimg;
+    pl_type = p / a.nimg;
+    const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
+    const uint8_t* img = a.rgb + (size_t)n * a.H0 * a.W0 * 3;
+#pragma unroll
+    for (int j = 0; j < NRGB; ++j) {
+      const int idx = tid1 + 256 * j;
+      const int r = idx / C12_PH, c = idx - r * C12_PH;
+      const int gy = py0 + r, gx = px0 + c;
+      const bool inside = idx < C12_PH * C12_PH && (unsigned)gy < (unsigned)a.H0 && (unsigned)gx < (unsigned)a.W0;
+      const int cy = min(max(gy, 0), a.H0 - 1), cx = min(max(gx, 0), a.W0 - 1);
+      const uint8_t* px = img + ((size_t)cy * a.W0 + cx) * 3;
+      rgbv[j] = (uint32_t)px[0] | (uint32_t)px[1] << 8 | (uint32_t)px[2] << 16 | (inside ? 1u << 24 : 0u);
+    }
+  };
+  if constexpr (FUSE1) {
+    const f16x8* wa = (const f16x8*)a.wx1 + (size_t)model * 2 * 2 * 64 + lane;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) A1[ct][hl] = wa[(ct * 2 + hl) * 64];
+      b1[ct] = *(const f32x4*)(a.bias1 + model * 32 + 16 * ct + 4 * g);
+    }
+    scale1 = a.wscale1[model];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = 8 * g + j;
+      toff[j] = t < 25 ? (t / 5) * C12_PH + t % 5 : -1;
+    }
+    for (int q = threadIdx.x; q < 256; q += 64 * NW) lut[q] = c_u8_to_unit[q];
+    if constexpr (TS == 1)
+      if (ntile > 0) rgb_load(0);
+  }
+
   f32x4 acc[MT];
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
   int ep_p = 0, ep_y = 0, ep_x = 0;
-  if (ntile > 0) issue(0);
+  if constexpr (!FUSE1)
+    if (ntile > 0) issue(0);
   for (int i = 0; i <= ntile; ++i) {
     dma_wait_all();
     lds_reads_done();
@@ -1689,9 +1750,69 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       }
     }
     if (i == ntile) break;
-    if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
+    if constexpr (!FUSE1) {
+      if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
+    }
     tile_at(i, ep_p, ep_y, ep_x);
-    const char* buf = lds + (i & 1) * G::HALO_BYTES;
+    const char* buf = lds + (FUSE1 ? 0 : (i & 1)) * G::HALO_BYTES;
+    if constexpr (FUSE1) {
+      // colour plane of the patch (utils.py:74-77: x/255, ((r k0 + g k1) + b k2) + off, every op
+      // rounded), zero outside the image (conv1's SAME padding)
+      if constexpr (TS == 1) {
+        const float* kk = c_ycbcr + pl_type * 3;
+        const float off = c_ycbcr_off[pl_type];
+#pragma unroll
+        for (int j = 0; j < NRGB; ++j) {
+          const int idx = tid1 + 256 * j;
+          if (idx < C12_PH * C12_PH) {
+            const uint32_t v = rgbv[j];
+            plane[idx] = (v >> 24) ? __fadd_rn(project(kk, lut[v & 255], lut[(v >> 8) & 255], lut[(v >> 16) & 255]), off)
+                                   : 0.f;
+          }
+        }
+      }
+      lds_reads_done();
+      stage_barrier();  // patch complete
+      // conv1 on the 19 x 19 halo pixels: px-tiles of 16, two 16-channel tiles each
+      char* halo = lds;
+      const int c1y0 = 2 * ep_y - a.pad_y, c1x0 = 2 * ep_x - a.pad_x;  // halo origin, conv1-output coords
+      for (int pt = wave; pt < (G::HH * G::HW + 15) / 16; pt += NW) {
+        const int q = 16 * pt + l16;
+        const bool qv = q < G::HH * G::HW;
+        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
+        const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
+        const float* pb = plane + 2 * hy * C12_PH + 2 * hx;
+        f16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = toff[j] >= 0 ? pb[toff[j]] : 0.f;
+          const _Float16 hh = (_Float16)x;
+          bh[j] = hh;
+          bl[j] = (_Float16)(x - (float)hh);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          f32x4 c = {0.f, 0.f, 0.f, 0.f};
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh, c, 0, 0, 0);  // w_lo*a_hi
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl, c, 0, 0, 0);  // w_hi*a_lo
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh, c, 0, 0, 0);  // w_hi*a_hi
+          f32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(__fadd_rn(__fmul_rn(c[r], scale1), b1[ct][r])) : 0.f;
+          f16x4 hi, lo;
+          split4(v, hi, lo);
+          if (qv) {
+            char* d = halo + hy * G::RPB + G::col(hx) * G::PSB + (16 * ct + 4 * g) * 2;
+            *(f16x4*)d = hi;
+            *(f16x4*)(d + CIN * 2) = lo;
+          }
+        }
+      }
+      if constexpr (TS == 1)
+        if (i + 1 < ntile) rgb_load(i + 1);  // in flight during this tile's conv2 MFMAs
+      lds_reads_done();
+      stage_barrier();  // halo complete
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // NT taps x KST k32-steps x MT pixel tiles, B fragments read DEPTH groups ahead
@@ -1728,19 +1849,21 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   }
 }
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1>
 __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
   using G = GeomS2<CIN, TH, 8>;
   constexpr int NCG = COUT / 16;
   static_assert(NCG * NTS == 8, "8 waves per block");
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 2 * (NTS - 1) * NCG * (TH / 2) * 1024];
+  constexpr int PARTS = 2 * (NTS - 1) * NCG * (TH / 2) * 1024;
+  __shared__ __attribute__((aligned(16)))
+  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PH + 256) * 4 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
-    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS>(a, lds, gi, bi, nb);
+    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS, FUSE1>(a, lds, gi, bi, nb);
   });
 }
 
@@ -2607,7 +2730,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
 
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
 // proportion to their planes.
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false>
 static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.tiles_y = (a.OH + TH - 1) / TH;
   a.tiles_x = (a.OW + 7) / 8;
@@ -2626,8 +2749,15 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = (int)by;
   a.ws_blk[2] = (int)(by + bc);
-  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   return hipGetLastError();
+}
+
+bool conv12_fused() { return use_ws(); }
+
+hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st) {
+  if (!a.rgb || !a.wx1 || !a.bias1 || a.H0 <= 0 || a.W0 <= 0) return hipErrorInvalidValue;
+  return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
 }
 
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {

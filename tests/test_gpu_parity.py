@@ -237,7 +237,10 @@ def test_layer_timing(codecs):
         c.decode(c.encode(x))
     t = c.layer_times()
     c.set_timing(False)
-    assert all(n == 3 and ms > 0 for ms, n in t.values())
+    # f16x3 runs conv1 inside conv2's kernel (no launch of its own); fp32 launches it
+    fused = c.precision == "f16x3"
+    assert t["conv1"][1] == (0 if fused else 3)
+    assert all(n == 3 and ms > 0 for name, (ms, n) in t.items() if name != "conv1")
 
 
 def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden):
