@@ -32,6 +32,7 @@
 
 #include "nic_kernels.h"
 
+
 namespace nic {
 
 static int device_cus();  // CUs of the current device (cached)
@@ -1519,6 +1520,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
       fb[m][0] = *(const f16x8*)(buf + boff[m] + step_off(0));
       fb[m][1] = *(const f16x8*)(buf + boff[m] + step_off(0) + CIN * 2);
     }
+    __builtin_amdgcn_s_setprio(1);  // the MFMA stream outranks the partner wave's epilogue / DMA issue
 #pragma unroll
     for (int st = 0; st < NSTEP; ++st) {
       const int t = st / KST, ks = st - t * KST;
@@ -1535,6 +1537,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
       }
     }
+    __builtin_amdgcn_s_setprio(0);
   }
 #ifdef NIC_STAMPS
   if (threadIdx.x == 0) {
