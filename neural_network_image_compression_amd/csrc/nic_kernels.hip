@@ -68,8 +68,7 @@ __device__ unsigned long long* g_stamps;
       g_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                       \
   } while (0)
-// pipelined kernels: cycle sums per block, g_stamps[blk * 8 + k] (k 0..3 consumer wave 0,
-// 4..7 first producer wave)
+// persistent kernels: per-block cycle sums (tools/ws_stamps.cpp, tools/d8_stamps.cpp)
 #define NIC_PNOW(v)                    \
   do {                                 \
     __builtin_amdgcn_sched_barrier(0); \
@@ -414,10 +413,6 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 // NIC_DMA_STAGE=1: one-tile-per-block kernels stage split halos by LDS-DMA instead of VGPRs
 #ifndef NIC_DMA_STAGE
 #define NIC_DMA_STAGE 0
-#endif
-// NIC_PPRIO=1: loader waves of the pipelined kernels run at s_setprio 2
-#ifndef NIC_PPRIO
-#define NIC_PPRIO 1
 #endif
 #if NIC_PIN
 #define NIC_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -952,13 +947,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 }
 
 // ------------------------------------------------------------------------------------
-// Pipelined persistent x3 conv.  One block per CU loops over tiles; wave NCW is a
-// producer that DMAs stage k+1 (a tile's halo, or a CCH-channel slice of it) into one LDS
-// buffer while the NCW consumer waves (one per SIMD) run the MFMAs of stage k from the
-// other.  One s_barrier per stage and no memory fence, so the consumers' weight prefetch
-// and output stores stay in flight across stage boundaries (the producer alone drains its
-// DMAs with vmcnt(0) before arriving).  Consumers cover all COUT channels of MTW M tiles:
-// every A fragment read from LDS feeds 3 * COUT/32 MFMAs.
+// Persistent-kernel helpers: a tile barrier that is not a memory fence, and LDS-DMA halo
+// pieces (HaloPieces) shared by the weight-stationary kernels.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void stage_barrier() {
   asm volatile("" ::: "memory");  // no LDS access moves across (s_barrier itself is not a fence)
@@ -968,77 +958,6 @@ __device__ __forceinline__ void stage_barrier() {
 // lgkmcnt(0) (vmcnt 63, expcnt 7): this wave's LDS reads of the stage buffer have returned
 __device__ __forceinline__ void lds_reads_done() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
-// DMA one stage: channel slice c (CCH channels) of the split halo of plane p into buf.
-// LDS pixel record = [hi CCH | lo CCH | pad]; pad slots and row padding are never read, so
-// those lanes issue nothing; out-of-image pixels load zeros.
-template <class G, int CIN, int CCH, int NPW>
-__device__ __forceinline__ void dma_stage(char* buf, const ConvArgs& a, int p, int gy0, int gx0, int c, int pw,
-                                          int lane) {
-  constexpr int PSS = G::PSB / 16, RPS = G::RPB / 16, HS = CCH / 8;
-  constexpr int TOTAL = G::HH * RPS;
-  const char* base = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
-#pragma unroll 2
-  for (int q0 = pw * 64; q0 < TOTAL; q0 += NPW * 64) {
-    const int q = q0 + lane;
-    const int row = q / RPS, r = q - row * RPS;
-    const int sp = r / PSS, k = r - sp * PSS;
-    if (q < TOTAL && sp < G::HW && k < PSS - 1) {
-      const int hx = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
-      const int gy = gy0 + row, gx = gx0 + hx;
-      const bool valid = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-      const int gslot = k < HS ? c * HS + k : CIN / 8 + c * HS + (k - HS);
-      dma16(valid ? base + ((size_t)gy * a.W + gx) * (CIN * 4) + gslot * 16 : a.zero16, buf + q0 * 16);
-    }
-  }
-}
-
-// One tap of one stage, term-major: the three split products of every (i, j) tile are
-// issued as 3 rounds over the MTW x NTW accumulators (independent MFMAs back to back; each
-// accumulator still sees w_lo*a_hi, w_hi*a_lo, w_hi*a_hi in that order, as in mma_tap_x3).
-template <int MTW, int NTW, int NS, int CCH>
-__device__ __forceinline__ void mma_tap_p(f32x16 (&acc)[MTW][NTW], const f16x8 (&b)[NS][2][NTW], const char* lds,
-                                          const int (&a_off)[MTW], int toff, int toff_next, f16x8 (&ahi0)[MTW],
-                                          f16x8 (&alo0)[MTW]) {
-  f16x8 ahi1[MTW], alo1[MTW];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    f16x8(&chi)[MTW] = (s & 1) ? ahi1 : ahi0;
-    f16x8(&clo)[MTW] = (s & 1) ? alo1 : alo0;
-    f16x8(&nhi)[MTW] = (s & 1) ? ahi0 : ahi1;
-    f16x8(&nlo)[MTW] = (s & 1) ? alo0 : alo1;
-    load_a_x3<MTW, CCH>(nhi, nlo, lds, a_off, s + 1 < NS ? toff + (s + 1) * 32 : toff_next);
-    NIC_FENCE();
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][1][j], chi[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], chi[i], acc[i][j], 0, 0, 0);
-    NIC_FENCE();
-  }
-  if constexpr (NS % 2 == 1) {
-#pragma unroll
-    for (int i = 0; i < MTW; ++i) {
-      ahi0[i] = ahi1[i];
-      alo0[i] = alo1[i];
-    }
-  }
-}
-
-// Loader-side geometry of a halo stage, computed once per loader wave: piece i of this
-// wave (LDS slots q0 = (pw + i*NPW)*64 ..) maps lane -> halo row, halo column and record
-// slot, packed as row | hx << 8 | slot << 16 | (slot is read) << 24.  Per stage a piece
-// then costs a few VALU: no divisions, no branches (lanes whose slot is never read, or
-// whose pixel is outside the image, load the zero block).
 template <class G, int CIN, int CCH, int NPW>
 struct HaloPieces {
   static constexpr int PSS = G::PSB / 16, RPS = G::RPB / 16, HS = CCH / 8;
@@ -1073,247 +992,6 @@ struct HaloPieces {
     }
   }
 };
-
-struct PipeTile {
-  int p, t0y, t0x, model;
-};
-
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int MTW, int NCW, int NPW, int CCH, bool WL,
-          int OUT_MODE, bool RESID>
-__global__ __launch_bounds__(64 * (NCW + NPW)) void conv_pipe_kernel(ConvArgs a) {
-  using G = GeomX3<CCH, COUT, KS, S, TR, TH, TW, NCW, 1, 1, MTW>;
-  constexpr int NCH = CIN / CCH;  // stages per tile
-  constexpr int NSC = CCH / 16;   // k16 steps per tap and stage
-  constexpr int NTW = COUT / 32;
-  constexpr int NTAPS = KS * KS;
-  constexpr int TAP_BYTES = CIN * COUT * 4;
-  constexpr int CHUNK_BYTES = NSC * 2 * 2 * COUT * 16;  // a stage's slice of one tap's weights
-  static_assert(CIN % CCH == 0, "channel slices");
-  static_assert(!TR || NCH == 1, "transposed: the phase accumulators need all of Cin in one stage");
-  // WL: the stage buffer also holds the stage's weight slice (NTAPS x CHUNK_BYTES, copied
-  // verbatim from wx by the loaders), so consumers issue no global loads in the tap loop
-  constexpr int W_BYTES = WL ? NTAPS * CHUNK_BYTES : 0;
-  constexpr int BUF = G::HALO_BYTES + W_BYTES;
-  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
-
-  const int nblk = gridDim.x, blk = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, half = lane >> 5;
-  // iteration i covers tiles [i*nblk, (i+1)*nblk); the blocks of one XCD (blk % 8) take a
-  // contiguous range of it, so neighbouring tiles (shared halo rows) meet in the same L2
-  const bool xcd = nblk % 8 == 0;
-  auto tile_of = [&](int i) { return xcd ? i * nblk + (blk & 7) * (nblk >> 3) + (blk >> 3) : i * nblk + blk; };
-  const int niter = (a.ntiles + nblk - 1) / nblk;
-  const int ntile = niter - (niter > 0 && tile_of(niter - 1) >= a.ntiles ? 1 : 0);  // a prefix of the i's
-  const int nst = ntile * NCH;
-  const int per_plane = a.tiles_y * a.tiles_x;
-  auto decode = [&](int st) {
-    const int t = tile_of(st / NCH);
-    PipeTile pt;
-    pt.p = t / per_plane;
-    const int r = t - pt.p * per_plane, ty = r / a.tiles_x;
-    pt.t0y = ty * TH;
-    pt.t0x = (r - ty * a.tiles_x) * TW;
-    pt.model = pt.p >= a.nimg ? 1 : 0;
-    return pt;
-  };
-  auto halo_origin = [&](const PipeTile& pt, int& gy0, int& gx0) {
-    if constexpr (TR) {
-      gy0 = pt.t0y - 1;
-      gx0 = pt.t0x - 1;
-    } else {
-      gy0 = pt.t0y * S - a.pad_y;
-      gx0 = pt.t0x * S - a.pad_x;
-    }
-  };
-
-#ifdef NIC_STAMPS
-  unsigned long long pst[3] = {0, 0, 0}, pst0;
-  NIC_PNOW(pst0);
-#endif
-  if (wave >= NCW) {  // ---- producers: NPW waves share each stage's DMA pieces ----
-#if NIC_PPRIO
-    __builtin_amdgcn_s_setprio(2);  // loader issue wins arbitration against the MFMA waves
-#endif
-    HaloPieces<G, CIN, CCH, NPW> hp;
-    hp.init(wave - NCW, lane);
-    for (int st = 0; st <= nst; ++st) {
-      if (st < nst) {
-        const PipeTile pt = decode(st);
-        int gy0, gx0;
-        halo_origin(pt, gy0, gx0);
-        char* buf = lds + (st & 1) * BUF;
-        hp.issue(buf, (const char*)a.in_s + (size_t)pt.p * a.H * a.W * CIN * 4, a.zero16, a.H, a.W, gy0, gx0,
-                 st % NCH, wave - NCW);
-        if constexpr (WL) {
-          const char* wsrc = (const char*)a.wx + (size_t)pt.model * NTAPS * TAP_BYTES + (st % NCH) * CHUNK_BYTES;
-#pragma unroll 2
-          for (int q0 = (wave - NCW) * 64; q0 < W_BYTES / 16; q0 += NPW * 64) {
-            const int off = (q0 + lane) * 16, t = off / CHUNK_BYTES;
-            dma16(wsrc + (size_t)t * TAP_BYTES + (off - t * CHUNK_BYTES), buf + G::HALO_BYTES + q0 * 16);
-          }
-        }
-      }
-#ifdef NIC_STAMPS
-      unsigned long long t0, t1, t2;
-      NIC_PNOW(t0);
-#endif
-      dma_wait_all();
-#ifdef NIC_STAMPS
-      NIC_PNOW(t1);
-#endif
-      stage_barrier();  // stage st landed (st == 0: prologue); consumers now run stage st - 1 -> st
-#ifdef NIC_STAMPS
-      NIC_PNOW(t2);
-      pst[0] += t1 - t0;
-      pst[1] += t2 - t1;
-#endif
-    }
-#ifdef NIC_STAMPS
-    unsigned long long te;
-    NIC_PNOW(te);
-    if (wave == NCW && lane == 0) {
-      g_stamps[blk * 8 + 4] = pst[0];
-      g_stamps[blk * 8 + 5] = pst[1];
-      g_stamps[blk * 8 + 6] = te - pst0;
-      g_stamps[blk * 8 + 7] = nst;
-    }
-#endif
-    return;
-  }
-
-  // ---- consumers ----
-  int a_off[MTW], my[MTW], mx[MTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i) {
-    const int m = (wave * MTW + i) * 32 + (lane & 31);
-    my[i] = m / TW;
-    mx[i] = m - my[i] * TW;
-    a_off[i] = (TR || S == 1) ? G::pix_off(my[i], mx[i]) + half * 16
-                              : my[i] * 2 * G::RPB + mx[i] * G::PSB + half * 16;
-  }
-  auto tap_off = [&](int t) {
-    if constexpr (TR) {
-      constexpr unsigned long long kTabLo = 0x6251409518405140ull, kTabHi = 0xa62951840ull;  // see conv_x3_kernel
-      const int e = (int)((t < 16 ? kTabLo >> (4 * t) : kTabHi >> (4 * (t - 16))) & 15);
-      return (e & 3) * G::RPB + (e >> 2) * G::PSB;
-    } else {
-      const int kh = t / KS, kw = t - (t / KS) * KS;
-      return G::S2 ? kh * G::RPB + ((kw & 1) * G::HE + (kw >> 1)) * G::PSB : kh * G::RPB + kw * G::PSB;
-    }
-  };
-  const char* wlane = (const char*)a.wx + (half * COUT + (lane & 31)) * 16;
-  auto wstage = [&](int st) {  // this lane's weights of stage st, tap 0
-    const PipeTile pt = decode(st);
-    return wlane + (size_t)pt.model * NTAPS * TAP_BYTES + (st % NCH) * CHUNK_BYTES;
-  };
-  constexpr int T = TR ? 25 : NTAPS;  // taps per stage (transposed: 4 phases, 4+6+6+9)
-
-  f16x8 bc[NSC][2][NTW], bn[NSC][2][NTW];
-  f32x16 acc[MTW][NTW];
-  f32x4 bias4[NTW][4];
-  if constexpr (!WL) {
-    if (nst > 0) load_b_x3<NSC, NTW, COUT>(bc, wstage(0), 0);
-  }
-  stage_barrier();  // prologue: stage 0 landed
-
-  for (int st = 0; st < nst; ++st) {
-    const PipeTile pt = decode(st);
-    const int c = st % NCH;
-    const char* buf = lds + (st & 1) * BUF;
-    // this lane's B fragments of tap 0: LDS copy (WL) or the global weights; the tap after
-    // the last one is the next stage's tap 0 (global), or a harmless re-read (LDS)
-    const char* wst = WL ? buf + G::HALO_BYTES + (half * COUT + (lane & 31)) * 16 : wstage(st);
-    const char* wnext = (!WL && st + 1 < nst) ? wstage(st + 1) : wst + (size_t)(T - 1) * (WL ? CHUNK_BYTES : TAP_BYTES);
-    const float scale = a.wscale[pt.model];
-    if (c == 0) {
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          bias4[j][g] = *(const f32x4*)(a.bias + pt.model * COUT + j * 32 + 8 * g + 4 * half);
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
-    }
-    auto epilogue = [&](int py, int px) {
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int oy = TR ? 2 * (pt.t0y + my[i]) + py : pt.t0y + my[i];
-          const int ox = TR ? 2 * (pt.t0x + mx[i]) + px : pt.t0x + mx[i];
-          store_tile_t<COUT, OUT_MODE, RESID>(a, pt.p, j, acc[i][j], oy, ox, scale, bias4[j]);
-          acc[i][j] = (f32x16){};
-        }
-    };
-    // after tap t: transposed phase ends (taps 3, 9, 15, 24) -> that phase's epilogue
-    auto after_tap = [&](int t) {
-      if constexpr (TR) {
-        if (t == 3 || t == 9 || t == 15 || t == 24) {
-          const int ph = t == 3 ? 0 : t == 9 ? 1 : t == 15 ? 2 : 3;
-          epilogue(ph >> 1, ph & 1);
-        }
-      }
-    };
-    auto b_addr = [&](int t) { return t < T ? wst + (size_t)t * (WL ? CHUNK_BYTES : TAP_BYTES) : wnext; };
-    if constexpr (WL) load_b_x3<NSC, NTW, COUT>(bc, wst, 0);
-
-    f16x8 ahi[MTW], alo[MTW];
-    load_a_x3<MTW, CCH>(ahi, alo, buf, a_off, tap_off(0));
-#pragma unroll 1
-    for (int t = 0; t < T; t += 2) {
-      // tap t (B in bc), its successor's B requested first; tap t+1 (B in bn) likewise
-      load_b_x3<NSC, NTW, COUT>(bn, b_addr(t + 1), 0);
-      NIC_FENCE();
-      const int o1 = t + 1 < T ? tap_off(t + 1) : tap_off(t);
-      mma_tap_p<MTW, NTW, NSC, CCH>(acc, bc, buf, a_off, tap_off(t), o1, ahi, alo);
-      after_tap(t);
-      if (t + 1 < T) {
-        load_b_x3<NSC, NTW, COUT>(bc, b_addr(t + 2), 0);
-        NIC_FENCE();
-        const int o2 = t + 2 < T ? tap_off(t + 2) : o1;
-        mma_tap_p<MTW, NTW, NSC, CCH>(acc, bn, buf, a_off, o1, o2, ahi, alo);
-        after_tap(t + 1);
-      } else {
-#pragma unroll
-        for (int s = 0; s < NSC; ++s)
-#pragma unroll
-          for (int hl = 0; hl < 2; ++hl)
-#pragma unroll
-            for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
-      }
-    }
-#ifdef NIC_STAMPS
-    unsigned long long t0, t1, t2;
-    NIC_PNOW(t0);
-#endif
-    if constexpr (!TR) {
-      if (c == NCH - 1) epilogue(0, 0);
-    }
-#ifdef NIC_STAMPS
-    NIC_PNOW(t1);
-#endif
-    lds_reads_done();
-    stage_barrier();  // done with buf; stage st + 1 landed in the other one
-#ifdef NIC_STAMPS
-    NIC_PNOW(t2);
-    pst[0] += t2 - t1;
-    pst[1] += t1 - t0;
-#endif
-  }
-#ifdef NIC_STAMPS
-  unsigned long long te;
-  NIC_PNOW(te);
-  if (threadIdx.x == 0) {
-    g_stamps[blk * 8 + 0] = pst[0];
-    g_stamps[blk * 8 + 1] = pst[1];
-    g_stamps[blk * 8 + 2] = te - pst0;
-    g_stamps[blk * 8 + 3] = nst;
-  }
-#endif
-}
 
 // ------------------------------------------------------------------------------------
 // Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16) over a
@@ -2646,19 +2324,6 @@ static hipError_t launch_x3(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
-#ifndef NIC_NPW
-#define NIC_NPW 4  // producer (LDS-DMA loader) waves per pipelined block
-#endif
-// NIC_PIPE=1 selects the pipelined persistent kernels for the 3x3 layers and dconv7
-// (measured slower than the one-tile-per-block kernels on MI355X)
-static bool use_pipe() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_PIPE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 // NIC_WS=0 selects the one-tile-per-block kernels for the 3x3 layers instead of the
 // weight-stationary ones (A/B)
 static bool use_ws() {
@@ -2679,22 +2344,6 @@ static int device_cus() {
     cache[d] = n;
   }
   return cache[d];
-}
-
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int MTW, int NCW, int NPW, int CCH, bool WL,
-          int OUT_MODE, bool RESID>
-static hipError_t launch_pipe(ConvArgs a, hipStream_t st) {
-  const int gy = TR ? a.H : a.OH, gx = TR ? a.W : a.OW;
-  a.tiles_y = (gy + TH - 1) / TH;
-  a.tiles_x = (gx + TW - 1) / TW;
-  const long long nt = (long long)a.tiles_y * a.tiles_x * a.P;
-  if (nt == 0) return hipSuccess;
-  if (nt > INT32_MAX) return hipErrorInvalidValue;
-  a.ntiles = (int)nt;
-  const int grid = a.ntiles < device_cus() ? a.ntiles : device_cus();  // one resident block per CU
-  hipLaunchKernelGGL((conv_pipe_kernel<CIN, COUT, KS, S, TR, TH, TW, MTW, NCW, NPW, CCH, WL, OUT_MODE, RESID>),
-                     dim3(grid), dim3(64 * (NCW + NPW)), 0, st, a);
-  return hipGetLastError();
 }
 
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
@@ -2771,11 +2420,9 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
     case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
                    // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
-      if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_CONV4:
       if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
-      if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
     case L_CONV8:  // 64->32 k5 s2 -> latent: tap-split weight-stationary (2 channel groups x 4 tap
                    // quarters, 4x8 tiles), or 4x8 tile with taps split over 4 waves
@@ -2785,15 +2432,12 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
       return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
     case L_DCONV5:
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
-      if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     case L_DCONV6:
       if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
-      if (use_pipe()) return launch_pipe<64, 64, 3, 1, false, 16, 16, 1, 8, 4, 16, true, OUT_SPLIT, true>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
     case L_DCONV7:  // 64->64 transposed k5 s2: per-phase weight-stationary groups, or 8x16 coarse tiles
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, true>(a, st);
-      if (use_pipe()) return launch_pipe<64, 64, 5, 2, true, 8, 16, 1, 4, NIC_NPW, 64, false, OUT_SPLIT, false>(a, st);
       return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
     default:
       return hipErrorInvalidValue;

@@ -269,13 +269,14 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
 
 
-def test_pipelined_kernels_parity(tmp_path):
-    """The opt-in producer/consumer kernels (NIC_PIPE=1: 3x3 layers and dconv7) meet the
-    golden contract too; they run in a child process because the switch is read at load."""
+def test_alternative_kernels_parity(tmp_path):
+    """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
+    NIC_D8=tile) meet the golden contract too; they run in a child process because the
+    switches are read when the library loads."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, NIC_PIPE="1")
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pipe_check.py")
+    env = dict(os.environ, NIC_WS="0", NIC_D8="tile")
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
-    assert out.returncode == 0 and "PIPE-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+    assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]

@@ -1,5 +1,5 @@
 // Diagnostic harness (NOT part of the product): compiles the codec kernels with
-// NIC_STAMPS, runs one split-f16 conv layer on synthetic data at the config-2 shape and
+// NIC_STAMPS and NIC_WS=0 (the one-tile-per-block kernels), runs one split-f16 conv layer on synthetic data at the config-2 shape and
 // reports the average per-block cycles in halo staging / MFMA main loop / epilogue, and
 // the implied concurrency.  Build + run (GPU box):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNIC_STAMPS \
@@ -110,20 +110,6 @@ int main() {
     std::vector<unsigned long long> hs(blocks * 4);
     CK(hipMemcpy(hs.data(), st, blocks * 32, hipMemcpyDeviceToHost));
 
-    const bool pipe = use_pipe() && (c.id == L_CONV3 || c.id == L_CONV4 || c.id == L_DCONV7);
-    if (pipe) {  // persistent pipelined kernel: per-block cycle sums (see conv_pipe_kernel)
-      const int nb = std::min<size_t>(blocks, device_cus());
-      double cw = 0, ce = 0, cl = 0, pw = 0, pb = 0, pl = 0, ns = 0;
-      for (int b = 0; b < nb; ++b) {
-        cw += hs[b * 8 + 0]; ce += hs[b * 8 + 1]; cl += hs[b * 8 + 2]; ns += hs[b * 8 + 3];
-        pw += hs[b * 8 + 4]; pb += hs[b * 8 + 5]; pl += hs[b * 8 + 6];
-      }
-      printf("%-7s pipe %d blocks %.3f ms  stages/block %.1f  consumer: life %.0f  barrier-wait %.0f (%.0f%%)  "
-             "epilogue %.0f (%.0f%%)  | producer: life %.0f  dma-wait %.0f (%.0f%%)  barrier-wait %.0f (%.0f%%)  "
-             "| per stage: consumer busy %.0f cyc\n",
-             c.name, nb, ms, ns / nb, cl / nb, cw / nb, 100 * cw / cl, ce / nb, 100 * ce / cl, pl / nb, pw / nb,
-             100 * pw / pl, pb / nb, 100 * pb / pl, (cl - cw - ce) / ns);
-    }
     double s01 = 0, s12 = 0, s23 = 0;
     unsigned long long t_min = ~0ull, t_max = 0;
     for (size_t b = 0; b < blocks; ++b) {
@@ -134,7 +120,7 @@ int main() {
       t_max = std::max(t_max, hs[b * 4 + 3]);
     }
     const double span = (double)(t_max - t_min), life = (s01 + s12 + s23) / blocks;
-    if (!pipe) printf("%-7s blocks %6zu  %.3f ms  cycles/block: staging %7.0f  mfma %7.0f  epilogue %6.0f  "
+    printf("%-7s blocks %6zu  %.3f ms  cycles/block: staging %7.0f  mfma %7.0f  epilogue %6.0f  "
            "(%.0f%% / %.0f%% / %.0f%%)  concurrent blocks/CU %.2f\n",
            c.name, blocks, ms, s01 / blocks, s12 / blocks, s23 / blocks, 100 * s01 / blocks / life,
            100 * s12 / blocks / life, 100 * s23 / blocks / life, life * blocks / span / 256.0);
