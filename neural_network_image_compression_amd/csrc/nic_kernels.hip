@@ -1972,8 +1972,9 @@ __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
 // resident -- compute output row y from ring rows y-1..y+1.  Their clipped phase values
 // meet in LDS and the fourth wave runs the inverse colour transform + quantiser of row y-1.
 // LDS row slot: [plane][18 px][16 slots of 16 B] = the HBM pixel record [hi 64 | lo 64]
-// with slot s stored at s ^ (px & 15): the B-fragment reads (lane (g, l16) = pixel l16,
-// slot 4c + g [+ 8]) then hit 16 distinct slots per ds_read_b128 group, with no padding.
+// with slot s stored at s ^ (2 px & 15): the B-fragment reads (lane (g, l16) = pixel
+// l16 + dx, slot 4c + g [+ 8]) then hit 16 distinct slots per ds_read_b128 group for every
+// neighbour column dx (exhaustive search; s ^ (px & 15) collides for odd dx), no padding.
 // ------------------------------------------------------------------------------------
 #ifndef NIC_D8S_R
 #define NIC_D8S_R 5
@@ -2003,7 +2004,7 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
 
   // ---- loading, shared by the four waves: wave w DMAs pieces w, w+4, ... of every row ----
   // piece k: LDS slot q = 64k + lane -> (plane, px, stored slot s'); source = HBM slot
-  // s' ^ (px & 15) of pixel (row, x0 - 1 + px) of that plane
+  // s' ^ (2 px & 15) of pixel (row, x0 - 1 + px) of that plane
   constexpr int NPW = (D8S_PIECES + 3) / 4;
   const int npw = (D8S_PIECES - wave + 3) / 4;  // this wave's pieces per row (NPW or NPW-1)
   long long src[NPW];
@@ -2011,7 +2012,7 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
   for (int j = 0; j < NPW; ++j) {
     const int q = 64 * (wave + 4 * j) + lane;
     const int pl = q / (D8S_PX * 16), r = q - pl * (D8S_PX * 16);
-    const int px = r >> 4, s = (r & 15) ^ (px & 15);
+    const int px = r >> 4, s = (r & 15) ^ ((2 * px) & 15);
     const int gx = x0 - 1 + px;
     src[j] = (q < 3 * D8S_PX * 16 && gx >= 0 && gx < a.W)
                  ? (long long)(pl * a.nimg + n) * plane_bytes + (long long)gx * 256 + s * 16
@@ -2110,7 +2111,7 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) {
         const int px = l16 + dx;
-        boff[dx][c][hl] = (wave * D8S_PX + px) * 256 + (((8 * hl + 4 * c + g) ^ (px & 15)) * 16);
+        boff[dx][c][hl] = (wave * D8S_PX + px) * 256 + (((8 * hl + 4 * c + g) ^ ((2 * px) & 15)) * 16);
       }
 #ifdef NIC_STAMPS
   unsigned long long sb = 0, si = 0, sm = 0, sw = 0, t0, t1, t2, t3, t4;
