@@ -139,9 +139,10 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
     out.assign(26 * 32, 0.f);
     for (int t = 0; t < 25; ++t)
       for (int co = 0; co < 32; ++co) out[t * 32 + co] = K[t * 32 + co];
-    // split-f16 MFMA A fragments of the fused conv1 (v_mfma_f32_16x16x32_f16, K = taps padded
-    // to 32): [co tile ct][hi,lo][lane][j], lane l holds row co = 16ct + (l & 15) and tap
-    // t = 8 (l >> 4) + j (zero for t >= 25), scaled by 2^k so every value is a normal f16 pair
+    // split-f16 MFMA A fragments of the fused conv1 (v_mfma_f32_16x16x32_f16): [co tile ct]
+    // [hi,lo][lane][j], lane l holds row co = 16ct + (l & 15) and k = 8 (l >> 4) + j, where
+    // k = 2 * pair + e, pair = kh * 3 + kw / 2, kw = 2 (pair % 3) + e (zero for kw = 5 and
+    // pair >= 15: 25 taps in 32 slots), scaled by 2^k so every value is a normal f16 pair
     float maxabs = 0.f;
     for (int i = 0; i < 25 * 32; ++i) maxabs = std::max(maxabs, std::fabs(K[i]));
     int kexp = 0;
@@ -154,9 +155,10 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
     for (int ct = 0; ct < 2; ++ct)
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
-          const int t = 8 * (lane >> 4) + j, co = 16 * ct + (lane & 15);
-          if (t >= 25) continue;
-          const float w = std::ldexp(K[t * 32 + co], kexp);
+          const int kk = 8 * (lane >> 4) + j, pr = kk >> 1, kh = pr / 3, kw = 2 * (pr % 3) + (kk & 1);
+          const int co = 16 * ct + (lane & 15);
+          if (pr >= 15 || kw >= 5) continue;
+          const float w = std::ldexp(K[(kh * 5 + kw) * 32 + co], kexp);
           const _Float16 hi = (_Float16)w;
           const _Float16 lo = (_Float16)(w - (float)hi);
           std::memcpy(&outx[(((size_t)ct * 2 + 0) * 64 + lane) * 8 + j], &hi, 2);

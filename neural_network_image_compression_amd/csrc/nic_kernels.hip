@@ -37,6 +37,7 @@ namespace nic {
 
 static int device_cus();  // CUs of the current device (cached)
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1 (register arrays
 // indexed by I stay registers however large the body; #pragma unroll may give up).
@@ -1258,11 +1259,15 @@ struct GeomS2 {
 // conv1 fused into conv2 (FUSE1): per tile the 41 x 41 colour-plane patch conv1's 19 x 19
 // halo outputs need is computed from the RGB bytes (loaded into registers by the ts = 1
 // waves while the previous tile's MFMAs run), conv1 runs on the same split-f16 MFMA
-// (K = 25 taps padded to 32; B = im2col gathered from the patch, split on the fly) and its
+// (K = 25 taps as 15 (kh, kw pair) slots padded to 32: each lane's 8 taps are 4 8-B patch
+// reads; B = that im2col, split on the fly) and its
 // bias + leaky + split outputs land directly in the conv2 halo (zero outside conv1's output,
 // conv2's SAME padding).  The halo and the patch are single LDS buffers: each tile runs
 // [epilogue(i-1) | patch(i)] -> barrier -> conv1(i) -> barrier -> conv2 MFMAs(i).
 constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
+// patch row pitch in LDS (floats): columns 41..51 stay zero, so the tap pairs (kw 4, 5) of
+// the last column read a finite 0 for the zero weight of kw = 5
+constexpr int C12_PP = 52;
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
@@ -1276,7 +1281,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
   char* part = lds + (FUSE1 ? 1 : 2) * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
   float* plane = (float*)(part + 2 * (NTS - 1) * NCG * PART);  // FUSE1: colour-plane patch
-  float* lut = plane + C12_PH * C12_PH;                        // FUSE1: u8 -> fp32 / 255
+  float* lut = plane + C12_PH * C12_PP;                        // FUSE1: u8 -> fp32 / 255
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -1340,12 +1345,14 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   // patch (-1: pad tap >= 25), and the RGB bytes of the next patch (ts = 1 waves) ----
   f16x8 A1[2][2];
   f32x4 b1[2];
-  int toff[8];
+  int toff[4];  // patch offsets of this lane's 4 tap pairs (k = 2 * pair + e: pair = kh * 3 + kw / 2)
   float scale1 = 1.f;
   constexpr int NRGB = (C12_PH * C12_PH + 255) / 256;  // patch pixels per ts = 1 thread
-  uint32_t rgbv[NRGB];  // r | g << 8 | b << 16 | inside << 24 (used by the ts = 1 waves)
+  uint32_t rgb_b[NRGB][2];  // raw bytes of this thread's patch pixels (ts = 1 waves): r | g << 8, b
+  uint32_t rgb_in = 0;      // bit j: pixel j lies inside the image
   const int tid1 = (int)threadIdx.x - 256;
-  int pl_type = 0;  // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgbv
+  int pl_type = 0;  // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
+  // plain loads, unpacked only by the next tile's patch phase (no wait before the MFMAs)
   auto rgb_load = [&](int i) {
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
@@ -1353,6 +1360,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     pl_type = p / a.nimg;
     const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
     const uint8_t* img = a.rgb + (size_t)n * a.H0 * a.W0 * 3;
+    rgb_in = 0;
 #pragma unroll
     for (int j = 0; j < NRGB; ++j) {
       const int idx = tid1 + 256 * j;
@@ -1361,7 +1369,9 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       const bool inside = idx < C12_PH * C12_PH && (unsigned)gy < (unsigned)a.H0 && (unsigned)gx < (unsigned)a.W0;
       const int cy = min(max(gy, 0), a.H0 - 1), cx = min(max(gx, 0), a.W0 - 1);
       const uint8_t* px = img + ((size_t)cy * a.W0 + cx) * 3;
-      rgbv[j] = (uint32_t)px[0] | (uint32_t)px[1] << 8 | (uint32_t)px[2] << 16 | (inside ? 1u << 24 : 0u);
+      rgb_b[j][0] = *(const uint16_t*)px;  // r, g (unaligned 2-B load)
+      rgb_b[j][1] = px[2];
+      rgb_in |= (inside ? 1u : 0u) << j;
     }
   };
   if constexpr (FUSE1) {
@@ -1374,11 +1384,12 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
     scale1 = a.wscale1[model];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int t = 8 * g + j;
-      toff[j] = t < 25 ? (t / 5) * C12_PH + t % 5 : -1;
+    for (int j = 0; j < 4; ++j) {
+      const int pr = 4 * g + j;
+      toff[j] = pr < 15 ? (pr / 3) * C12_PP + 2 * (pr % 3) : -1;
     }
     for (int q = threadIdx.x; q < 256; q += 64 * NW) lut[q] = c_u8_to_unit[q];
+    for (int q = threadIdx.x; q < C12_PH * C12_PP; q += 64 * NW) plane[q] = 0.f;  // pad columns
     if constexpr (TS == 1)
       if (ntile > 0) rgb_load(0);
   }
@@ -1388,10 +1399,26 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   int ep_p = 0, ep_y = 0, ep_x = 0;
   if constexpr (!FUSE1)
     if (ntile > 0) issue(0);
+#ifdef NIC_STAMPS
+  unsigned long long sx[8] = {}, sa, sb;
+  NIC_PNOW(sa);
+#define WS2_MARK(kk)      \
+  do {                    \
+    NIC_PNOW(sb);         \
+    sx[kk] += sb - sa;    \
+    sa = sb;              \
+  } while (0)
+#else
+#define WS2_MARK(kk) \
+  do {               \
+  } while (0)
+#endif
   for (int i = 0; i <= ntile; ++i) {
+    WS2_MARK(6);  // conv2 MFMAs + partials (previous iteration)
     dma_wait_all();
     lds_reads_done();
     stage_barrier();  // halo of tile i complete; partials of tile i-1 written
+    WS2_MARK(0);      // top barrier
     if constexpr (TS == 0) {
       if (i > 0) {  // epilogue of tile i-1: own sums + the other tap groups' partials
         const char* pp = part + (((i - 1) & 1) * (NTS - 1) * NCG + cg) * PART + lane * 16;
@@ -1446,40 +1473,65 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         for (int j = 0; j < NRGB; ++j) {
           const int idx = tid1 + 256 * j;
           if (idx < C12_PH * C12_PH) {
-            const uint32_t v = rgbv[j];
-            plane[idx] = (v >> 24) ? __fadd_rn(project(kk, lut[v & 255], lut[(v >> 8) & 255], lut[(v >> 16) & 255]), off)
-                                   : 0.f;
+            const int r = idx / C12_PH, c = idx - r * C12_PH;
+            plane[r * C12_PP + c] = ((rgb_in >> j) & 1)
+                                        ? __fadd_rn(project(kk, lut[rgb_b[j][0] & 255], lut[rgb_b[j][0] >> 8], lut[rgb_b[j][1]]), off)
+                                        : 0.f;
           }
         }
       }
+      WS2_MARK(1);  // epilogue (ts 0) / patch (ts 1)
       lds_reads_done();
       stage_barrier();  // patch complete
+      WS2_MARK(2);
       // conv1 on the 19 x 19 halo pixels: px-tiles of 16, two 16-channel tiles each
       char* halo = lds;
       const int c1y0 = 2 * ep_y - a.pad_y, c1x0 = 2 * ep_x - a.pad_x;  // halo origin, conv1-output coords
-      for (int pt = wave; pt < (G::HH * G::HW + 15) / 16; pt += NW) {
+      // three px-tiles per wave, software-pipelined: all patch reads, then the splits, then
+      // six independent MFMA chains, then the epilogues
+      constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + NW - 1) / NW;
+      f32x2 xv[PTW][4];
+#pragma unroll
+      for (int u = 0; u < PTW; ++u) {
+        const int q = 16 * (wave + NW * u) + l16;
+        const int qq = q < G::HH * G::HW ? q : 0;
+        const int hy = qq / G::HW, hx = qq - hy * G::HW;
+        const float* pb = plane + 2 * hy * C12_PP + 2 * hx;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[u][j] = toff[j] >= 0 ? *(const f32x2*)(pb + toff[j]) : (f32x2){0.f, 0.f};
+      }
+      f16x8 bh[PTW], bl[PTW];
+#pragma unroll
+      for (int u = 0; u < PTW; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = xv[u][j >> 1][j & 1];
+          const _Float16 hh = (_Float16)x;
+          bh[u][j] = hh;
+          bl[u][j] = (_Float16)(x - (float)hh);
+        }
+      f32x4 c1[PTW][2];
+#pragma unroll
+      for (int u = 0; u < PTW; ++u)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl[u], c1[u][ct], 0, 0, 0);
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh[u], c1[u][ct], 0, 0, 0);
+        }
+#pragma unroll
+      for (int u = 0; u < PTW; ++u) {
+        const int pt = wave + NW * u;
+        if (pt >= NPT) break;  // wave-uniform
         const int q = 16 * pt + l16;
         const bool qv = q < G::HH * G::HW;
         const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
         const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
-        const float* pb = plane + 2 * hy * C12_PH + 2 * hx;
-        f16x8 bh, bl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = toff[j] >= 0 ? pb[toff[j]] : 0.f;
-          const _Float16 hh = (_Float16)x;
-          bh[j] = hh;
-          bl[j] = (_Float16)(x - (float)hh);
-        }
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          f32x4 c = {0.f, 0.f, 0.f, 0.f};
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh, c, 0, 0, 0);  // w_lo*a_hi
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl, c, 0, 0, 0);  // w_hi*a_lo
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh, c, 0, 0, 0);  // w_hi*a_hi
           f32x4 v;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(__fadd_rn(__fmul_rn(c[r], scale1), b1[ct][r])) : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(__fadd_rn(__fmul_rn(c1[u][ct][r], scale1), b1[ct][r])) : 0.f;
           f16x4 hi, lo;
           split4(v, hi, lo);
           if (qv) {
@@ -1489,10 +1541,13 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
           }
         }
       }
+      WS2_MARK(3);  // conv1
       if constexpr (TS == 1)
         if (i + 1 < ntile) rgb_load(i + 1);  // in flight during this tile's conv2 MFMAs
+      WS2_MARK(4);
       lds_reads_done();
       stage_barrier();  // halo complete
+      WS2_MARK(5);
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -1528,6 +1583,15 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
     }
   }
+#ifdef NIC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) o[q] = sx[q];
+    o[7] = ntile;
+  }
+#endif
+#undef WS2_MARK
 }
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1>
@@ -1537,7 +1601,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   static_assert(NCG * NTS == 8, "8 waves per block");
   constexpr int PARTS = 2 * (NTS - 1) * NCG * (TH / 2) * 1024;
   __shared__ __attribute__((aligned(16)))
-  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PH + 256) * 4 : 0)];
+  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PP + 256) * 4 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];

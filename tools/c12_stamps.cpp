@@ -1,0 +1,99 @@
+// Diagnostic harness (NOT part of the product): the fused conv1+conv2 kernel built with
+// NIC_STAMPS at the config-2 shape; per wave, cycle sums (s_memtime) per tile in: top
+// barrier, epilogue (ts 0) / colour patch (ts 1), patch barrier, conv1, RGB prefetch issue,
+// halo barrier, conv2 MFMAs + partials.  Build + run (GPU box):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNIC_STAMPS \
+//     -I neural_network_image_compression_amd/csrc tools/c12_stamps.cpp -o /tmp/c12 && /tmp/c12
+#include "../neural_network_image_compression_amd/csrc/nic_kernels.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace nic;
+
+#define CK(x)                                                \
+  do {                                                       \
+    hipError_t e = (x);                                      \
+    if (e != hipSuccess) {                                   \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); \
+      exit(1);                                               \
+    }                                                        \
+  } while (0)
+
+int main() {
+  const int N = 64, H0 = 256, W0 = 256, H1 = 128, W1 = 128, OH = 64, OW = 64, P = 3 * N;
+  float lut[256], k9[9] = {0.299f, 0.587f, 0.114f, -0.16874f, -0.33126f, 0.5f, 0.5f, -0.41869f, -0.08131f},
+                  off[3] = {0, .5f, .5f};
+  for (int i = 0; i < 256; ++i) lut[i] = i / 255.f;
+  CK(upload_constants(lut, k9, k9, off));
+  uint8_t* rgb;
+  uint16_t *out, *wx, *wx1;
+  float *bias, *bias1;
+  char* zero16;
+  CK(hipMalloc(&rgb, (size_t)N * H0 * W0 * 3));
+  std::vector<uint8_t> hr((size_t)N * H0 * W0 * 3);
+  for (auto& v : hr) v = rand() & 255;
+  CK(hipMemcpy(rgb, hr.data(), hr.size(), hipMemcpyHostToDevice));
+  CK(hipMalloc(&out, (size_t)P * OH * OW * 64 * 4));
+  CK(hipMalloc(&wx, (size_t)2 * 25 * 32 * 64 * 4));
+  CK(hipMemset(wx, 0x21, (size_t)2 * 25 * 32 * 64 * 4));
+  CK(hipMalloc(&wx1, 2 * 2 * 2 * 64 * 16));
+  CK(hipMemset(wx1, 0x21, 2 * 2 * 2 * 64 * 16));
+  CK(hipMalloc(&bias, 2 * 64 * 4));
+  CK(hipMemset(bias, 0, 2 * 64 * 4));
+  CK(hipMalloc(&bias1, 2 * 32 * 4));
+  CK(hipMemset(bias1, 0, 2 * 32 * 4));
+  CK(hipMalloc(&zero16, 256));
+  CK(hipMemset(zero16, 0, 256));
+  ConvArgs a{};
+  a.out_s = out;
+  a.zero16 = zero16;
+  a.wx = wx;
+  a.wscale[0] = a.wscale[1] = 1.f;
+  a.bias = bias;
+  a.P = P;
+  a.nimg = N;
+  a.H = H1;
+  a.W = W1;
+  a.OH = OH;
+  a.OW = OW;
+  a.pad_y = a.pad_x = 1;
+  a.rgb = rgb;
+  a.wx1 = wx1;
+  a.wscale1[0] = a.wscale1[1] = 1.f;
+  a.bias1 = bias1;
+  a.H0 = H0;
+  a.W0 = W0;
+  a.p1y = a.p1x = 1;
+  const int maxb = 1024;
+  unsigned long long* st;
+  CK(hipMalloc(&st, (size_t)maxb * 64 * 8));
+  CK(hipMemset(st, 0, (size_t)maxb * 64 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int it = 0; it < 20; ++it) CK(launch_conv12_x3(a, 0));
+  CK(hipEventRecord(e0, 0));
+  CK(launch_conv12_x3(a, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipDeviceSynchronize());
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> hs((size_t)maxb * 64);
+  CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
+  const char* nm[7] = {"top-bar", "epi/patch", "patch-bar", "conv1", "rgb-issue", "halo-bar", "mfma"};
+  printf("conv12 %.4f ms\n", ms);
+  for (int w = 0; w < 8; w += 4) {
+    double s[7] = {}, nt = 0;
+    for (int b = 0; b < maxb; ++b) {
+      if (hs[((size_t)b * 8 + w) * 8 + 7] == 0) continue;
+      for (int q = 0; q < 7; ++q) s[q] += hs[((size_t)b * 8 + w) * 8 + q];
+      nt += hs[((size_t)b * 8 + w) * 8 + 7];
+    }
+    printf("  wave %d (ts %d) per tile:", w, w / 4);
+    for (int q = 0; q < 7; ++q) printf("  %s %5.0f", nm[q], s[q] / nt);
+    printf("\n");
+  }
+  return 0;
+}
