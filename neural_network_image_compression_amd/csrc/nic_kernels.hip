@@ -86,6 +86,11 @@ __device__ __forceinline__ float leaky02(float z) {
   // tf.nn.leaky_relu(z, alpha=0.2) = max(alpha*z, z)
   return fmaxf(__fmul_rn(z, 0.2f), z);
 }
+// conv sum * 2^-k (exact: k undoes the power-of-two weight pre-scale of the split-f16
+// paths) + bias, rounded once -- bit-identical to TF's rounded BiasAdd of the fp32 sum
+__device__ __forceinline__ float scale_bias(float acc, float scale_pow2, float b) {
+  return __builtin_fmaf(acc, scale_pow2, b);
+}
 __device__ __forceinline__ float clip01(float v) {
   // tf.clip_by_value(v, 0, 1) = max(min(v, 1), 0)
   return fmaxf(fminf(v, 1.0f), 0.0f);
@@ -704,7 +709,7 @@ __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, c
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[g][q] = leaky02(__fadd_rn(__fmul_rn(acc[4 * g + q], scale), b[g][q]));
+    for (int q = 0; q < 4; ++q) v[g][q] = leaky02(scale_bias(acc[4 * g + q], scale, b[g][q]));
   if constexpr (OUT_MODE == OUT_SPLIT) {
     // every lane takes part in the swaps (EXEC must stay full); only in-image lanes store
     uint16_t* base = a.out_s + pix * COUT * 2 + nt * 32;
@@ -1152,7 +1157,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
         f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
+        for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
         if constexpr (RESID) {
           f16x4 rh, rl;
           unswap16(rq[m], rh, rl);
@@ -1433,7 +1438,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
           const int oy = ep_y + 2 * m + (l16 >> 3), ox = ep_x + (l16 & 7);
           f32x4 v;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = leaky02(__fadd_rn(__fmul_rn(acc[m][r], scale), bias[r]));
+          for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
           if constexpr (OUT_MODE == OUT_SPLIT) {
             f16x4 hi, lo;
             split4(v, hi, lo);
@@ -1531,7 +1536,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         for (int ct = 0; ct < 2; ++ct) {
           f32x4 v;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(__fadd_rn(__fmul_rn(c1[u][ct][r], scale1), b1[ct][r])) : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
           f16x4 hi, lo;
           split4(v, hi, lo);
           if (qv) {
@@ -1983,7 +1988,7 @@ __global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
       for (int i = 0; i < 4; ++i) {
         f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(__fadd_rn(__fmul_rn(acc[i][r], scale), b)));
+        for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(scale_bias(acc[i][r], scale, b)));
         res[(type * D8_TH + 2 * wave + (i >> 1)) * D8_TW + (i & 1) * 16 + lane] = v;
       }
     }
@@ -2224,7 +2229,7 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
     if (lane < 16) {  // D rows 0..3 (the phases) of pixel l16
       f32x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(__fadd_rn(__fmul_rn(acc[r], scale), bias)));
+      for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(scale_bias(acc[r], scale, bias)));
       ex[((y & 1) * 3 + wave) * D8S_W + l16] = v;
     }
     lds_reads_done();
