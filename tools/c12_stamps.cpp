@@ -1,6 +1,7 @@
 // Diagnostic harness (NOT part of the product): the fused conv1+conv2 kernel built with
 // NIC_STAMPS at the config-2 shape; per wave, cycle sums (s_memtime) per tile in: top
-// barrier, epilogue (ts 0), and the MFMA stream with its slotted conv1 / patch-DMA work.  Build + run (GPU box):
+// barrier, epilogue (ts 0) / colour patch (ts 1), patch barrier, conv1, RGB prefetch issue,
+// halo barrier, conv2 MFMAs + partials.  Build + run (GPU box):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNIC_STAMPS \
 //     -I neural_network_image_compression_amd/csrc tools/c12_stamps.cpp -o /tmp/c12 && /tmp/c12
 #include "../neural_network_image_compression_amd/csrc/nic_kernels.hip"
@@ -64,9 +65,6 @@ int main() {
   a.H0 = H0;
   a.W0 = W0;
   a.p1y = a.p1x = 1;
-  float* planes;
-  CK(hipMalloc(&planes, (size_t)3 * N * H0 * W0 * 4));
-  a.planes = planes;
   const int maxb = 1024;
   unsigned long long* st;
   CK(hipMalloc(&st, (size_t)maxb * 64 * 8));
@@ -84,7 +82,7 @@ int main() {
   CK(hipEventElapsedTime(&ms, e0, e1));
   std::vector<unsigned long long> hs((size_t)maxb * 64);
   CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
-  const char* nm[7] = {"top-bar", "epilogue", "stream", "-", "-", "-", "-"};
+  const char* nm[7] = {"top-bar", "epi/patch", "patch-bar", "conv1", "rgb-issue", "halo-bar", "mfma"};
   printf("conv12 %.4f ms\n", ms);
   for (int w = 0; w < 8; w += 4) {
     double s[7] = {}, nt = 0;
@@ -94,7 +92,7 @@ int main() {
       nt += hs[((size_t)b * 8 + w) * 8 + 7];
     }
     printf("  wave %d (ts %d) per tile:", w, w / 4);
-    for (int q = 0; q < 3; ++q) printf("  %s %5.0f", nm[q], s[q] / nt);
+    for (int q = 0; q < 7; ++q) printf("  %s %5.0f", nm[q], s[q] / nt);
     printf("\n");
   }
   return 0;
