@@ -58,14 +58,16 @@ enum {
   NIC_MODEL_DECODER_CBCR = 3
 };
 
-/* Arithmetic of the Cin >= 32 convolutions (conv2..conv8, dconv1..dconv7):
- *   NIC_PRECISION_FP32  -- exact-fp32 MFMA (v_mfma_f32_32x32x2_f32): an fp32 FMA chain;
- *   NIC_PRECISION_F16X3 -- split-f16 MFMA (default): each fp32 operand x = hi + lo with
- *     hi, lo f16 and weights pre-scaled by 2^k; a*w ~ a_hi*w_hi + a_hi*w_lo + a_lo*w_hi on
- *     v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Error ~2^-22 relative per product,
- *     i.e. at the level of fp32 accumulation-order differences; ~5x the fp32 MFMA rate.
- *     Requires |activations| < 65504 (f16 range).
- * conv1, dconv8, colour transforms and quantisers are fp32 in both modes. */
+/* Arithmetic of the convolutions:
+ *   NIC_PRECISION_FP32  -- exact-fp32 MFMA (v_mfma_f32_32x32x2_f32) for conv2..conv8 and
+ *     dconv1..dconv7: an fp32 FMA chain; conv1 and dconv8 as fp32 VALU FMA.
+ *   NIC_PRECISION_F16X3 -- split-f16 MFMA (default) for every convolution, conv1 (fused
+ *     into conv2's kernel) and dconv8 included: each fp32 operand x = hi + lo with hi, lo
+ *     f16 and weights pre-scaled by 2^k; a*w ~ a_hi*w_hi + a_hi*w_lo + a_lo*w_hi on
+ *     v_mfma_f32_16x16x32_f16 / v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Error
+ *     ~2^-22 relative per product, i.e. at the level of fp32 accumulation-order
+ *     differences.  Requires |activations| < 65504 (f16 range).
+ * Bias, activations, residuals, colour transforms and quantisers are fp32 in both modes. */
 enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
 
 /* ABI version: major * 10000 + minor * 100 + patch */
