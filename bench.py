@@ -205,17 +205,34 @@ def main():
     geo = layer_geometry(H, W)
     layers = {}
     conv1_fused = lt["conv1"][1] == 0 and lt["conv2"][1] > 0  # f16x3: conv1 runs inside conv2's kernel
+    # f16x3 with the weight-stationary kernels: dconv8's MACs run inside dconv7's kernel (the
+    # per-pixel tap projections); the dconv8 launch is then an HBM-bound gather (the library's
+    # rule, csrc/nic_kernels.hip dconv78_fused)
+    d78_fused = (args.precision == "f16x3" and os.environ.get("NIC_WS", "1")[:1] != "0"
+                 and os.environ.get("NIC_D8", "p")[:1] not in ("t", "s"))
+    moved = {"conv2": "conv1" if conv1_fused else None, "dconv7": "dconv8" if d78_fused else None}
     flops = {}
     for name, (ms, n) in lt.items():
         if n == 0:
             continue
         avg = ms / max(n, 1)
-        flop = flops[name] = (geo[name] + (geo["conv1"] if name == "conv2" and conv1_fused else 0)) * P
+        if name == "dconv8" and d78_fused:
+            # reads 25 fp32 projections per dconv7 output pixel, writes 3 B per output pixel
+            nbytes = P * (4 * h8) * (4 * w8) * 25 * 4 + B * (8 * h8) * (8 * w8) * 3
+            flops[name] = 0
+            layers[name] = {"avg_ms": round(avg, 4), "gbytes_per_launch": round(nbytes / 1e9, 3),
+                            "gbps": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None,
+                            "fused": "gather of dconv7's tap projections + inverse colour + quantiser"}
+            continue
+        extra = moved.get(name)
+        flop = flops[name] = (geo[name] + (geo[extra] if extra else 0)) * P
         layers[name] = {"avg_ms": round(avg, 4), "gflop_per_launch": round(flop / 1e9, 3),
                         "tflops": round(flop / (avg * 1e-3) / 1e12, 2) if avg > 0 else None}
         if name == "conv2" and conv1_fused:
             layers[name]["fused"] = "conv1 (colour transform + conv1 computed into conv2's LDS halo)"
-    dom = max(layers, key=lambda k: layers[k]["avg_ms"])
+        if name == "dconv7" and d78_fused:
+            layers[name]["fused"] = "dconv8's MACs (25 tap projections per output pixel, split-f16 MFMA)"
+    dom = max((k for k in layers if "tflops" in layers[k]), key=lambda k: layers[k]["avg_ms"])
     traffic = None
     if os.path.exists(args.traffic_json):
         try:

@@ -258,6 +258,8 @@ struct nic_ctx {
   float* wb[L_COUNT] = {};  // [2 models][cout]
   uint16_t* wx[L_COUNT] = {};  // split-f16 kernels [2 models][taps*cin*cout*2]
   float wscale[L_COUNT][2] = {};  // 2^-k per model for the split-f16 kernels
+  // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
+  uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
   char* zero16 = nullptr;  // 256 zero bytes: DMA source for halo padding
   bool have_k[4][5] = {};
@@ -322,7 +324,33 @@ struct DecGeom {
 };
 DecGeom dec_geom(int n, int h8, int w8) {
   const size_t P = 3 * (size_t)n;
-  return {P * (4 * (size_t)h8) * (4 * (size_t)w8) * 64, P * (2 * (size_t)h8) * (2 * (size_t)w8) * 64};
+  // R0: dconv7's output, or its dconv8 projections ([P][4 phases][8x8 tiles of the
+  // 2h8 x 2w8 coarse grid][25][64] floats, launch_dconv7_proj_x3)
+  const size_t t7 = (size_t)((2 * h8 + 7) / 8) * ((2 * w8 + 7) / 8);
+  const size_t r0 = std::max(P * (4 * (size_t)h8) * (4 * (size_t)w8) * 64, P * 4 * t7 * 25 * 64);
+  return {r0, P * (2 * (size_t)h8) * (2 * (size_t)w8) * 64};
+}
+constexpr size_t kProjFrag = 2 * 2 * 2 * 64 * 8;  // u16 per model in nic_ctx::wproj
+
+// dconv8's phase-tap kernel [25][64] (fp32 repack) as split-f16 B fragments of the
+// projection MFMA: lane l of (tap block nt, k32-step ks) holds column tap 16 nt + (l & 15)
+// and rows ci = 32 ks + 8 (l >> 4) + j, scaled by 2^kexp (zero for taps >= 25)
+std::vector<uint16_t> proj_fragments(const std::vector<float>& w25, int kexp) {
+  std::vector<uint16_t> f(kProjFrag, 0);
+  for (int nt = 0; nt < 2; ++nt)
+    for (int ks = 0; ks < 2; ++ks)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int tap = 16 * nt + (lane & 15);
+        if (tap >= 25) continue;
+        for (int j = 0; j < 8; ++j) {
+          const float w = std::ldexp(w25[(size_t)tap * 64 + 32 * ks + 8 * (lane >> 4) + j], kexp);
+          const _Float16 hi = (_Float16)w;
+          const _Float16 lo = (_Float16)(w - (float)hi);
+          std::memcpy(&f[((((size_t)nt * 2 + ks) * 2 + 0) * 64 + lane) * 8 + j], &hi, 2);
+          std::memcpy(&f[((((size_t)nt * 2 + ks) * 2 + 1) * 64 + lane) * 8 + j], &lo, 2);
+        }
+      }
+  return f;
 }
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -445,6 +473,10 @@ int nic_create(int device, nic_ctx** out) {
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
     }
   }
+  if (hipMalloc(&c->wproj, 2 * kProjFrag * 2) != hipSuccess || hipMemset(c->wproj, 0, 2 * kProjFrag * 2) != hipSuccess) {
+    nic_destroy(c);
+    return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
+  }
   if (hipMalloc(&c->zero16, 256) != hipSuccess || hipMemset(c->zero16, 0, 256) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: zero buffer allocation failed");
@@ -476,6 +508,7 @@ int nic_destroy(nic_ctx* c) {
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
   if (c->zero16) (void)hipFree(c->zero16);
+  if (c->wproj) (void)hipFree(c->wproj);
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
@@ -509,6 +542,10 @@ int nic_set_weights(nic_ctx* c, int model_id, const char* layer, const float* ho
       HIP_TRY(hipMemcpy(c->wx[L->id] + m * packedx.size(), packedx.data(), packedx.size() * sizeof(uint16_t),
                         hipMemcpyHostToDevice));
       c->wscale[L->id][m] = std::ldexp(1.0f, -kexp);
+    }
+    if (L->id == L_DCONV8) {
+      const std::vector<uint16_t> f = proj_fragments(packed, kexp);
+      HIP_TRY(hipMemcpy(c->wproj + m * kProjFrag, f.data(), f.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     }
     c->have_k[model_id][idx] = true;
   } else if (kind == "bias") {
@@ -687,7 +724,18 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   const int h2 = 2 * h8, w2 = 2 * w8;
   TIMED(L_DCONV5, run_layer(c, L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2), st));
   TIMED(L_DCONV6, run_layer(c, L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2), st));
-  TIMED(L_DCONV7, run_layer(c, L_DCONV7, conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2), st));
+  ConvArgs d7 = conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2);
+  // f16x3: dconv7 writes dconv8's per-pixel tap projections (100 B / pixel instead of 256)
+  const bool fuse78 = c->precision == NIC_PRECISION_F16X3 && dconv78_fused();
+  if (fuse78) {
+    d7.proj = R[0];
+    d7.proj_w = c->wproj;
+    d7.proj_scale[0] = c->wscale[L_DCONV8][0];
+    d7.proj_scale[1] = c->wscale[L_DCONV8][1];
+    TIMED(L_DCONV7, launch_dconv7_proj_x3(d7, st));
+  } else {
+    TIMED(L_DCONV7, run_layer(c, L_DCONV7, d7, st));
+  }
   Dconv8Args a8{};
   a8.in = R[0];
   a8.in_s = (const uint16_t*)R[0];
@@ -702,7 +750,14 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   a8.nimg = n;
   a8.H = 2 * h2;
   a8.W = 2 * w2;
-  TIMED(L_DCONV8, c->precision == NIC_PRECISION_F16X3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
+  if (fuse78) {
+    a8.proj = R[0];
+    a8.tiles_y7 = (h2 + 7) / 8;
+    a8.tiles_x7 = (w2 + 7) / 8;
+    TIMED(L_DCONV8, launch_dconv8_gather(a8, st));
+  } else {
+    TIMED(L_DCONV8, c->precision == NIC_PRECISION_F16X3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
+  }
   return NIC_OK;
 }
 

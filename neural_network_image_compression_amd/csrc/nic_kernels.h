@@ -49,6 +49,11 @@ struct ConvArgs {
   const float* bias1;     // [2][32]
   int H0, W0;             // image size (conv1 input)
   int p1y, p1x;           // conv1 TF-SAME pad_lo
+  // dconv8 projection fused into dconv7 (f16x3): per dconv7 output pixel the 25 phase-tap
+  // dot products with dconv8's kernel, tile-major [P][4 phases][tiles_y][tiles_x][25][64 px]
+  float* proj;
+  const uint16_t* proj_w;  // MFMA B fragments [2 models][2 tap blocks][Cin/32][hi,lo][64 lanes][8] of w8*2^k
+  float proj_scale[2];     // 2^-k per model
 };
 
 struct Conv1Args {
@@ -72,6 +77,8 @@ struct Dconv8Args {
   const float* bias;    // [2]
   int nimg, H, W, tiles_x;
   int strips, nseg, seg_rows;  // strip-walk kernel: column strips, row segments
+  const float* proj;           // gather kernel: dconv7's projections (ConvArgs::proj layout)
+  int tiles_y7, tiles_x7;      // gather kernel: dconv7's 8x8 tile grid over its coarse input
 };
 
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
@@ -82,6 +89,11 @@ bool conv12_fused();  // whether nic_encode uses launch_conv12_x3 in f16x3 mode
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);      // exact fp32 VALU
 hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st);   // split-f16 MFMA
+// f16x3 decoder tail with dconv8 split across two kernels: dconv7 writes the 25 projections
+// of every output pixel instead of its 64 channels, the gather sums them per output pixel
+bool dconv78_fused();
+hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st);
+hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st);
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 

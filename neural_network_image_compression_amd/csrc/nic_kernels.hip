@@ -983,14 +983,18 @@ struct HaloPieces {
       code[i] = read ? (row | hx << 8 | slot << 16 | 1 << 24) : 0;
     }
   }
-  // DMA channel slice c of plane base `base` (halo origin gy0, gx0) into buf
+  // DMA channel slice c of plane base `base` (halo origin gy0, gx0) into buf.  OPAQUE
+  // keeps the compiler from hoisting the decoded pieces out of the tile loop (64-bit
+  // offsets per piece: spills in register-tight kernels).
+  template <bool OPAQUE = false>
   __device__ __forceinline__ void issue(char* buf, const char* base, const char* zero16, int H, int W, int gy0,
                                         int gx0, int c, int pw) const {
 #pragma unroll
     for (int i = 0; i < NPP; ++i) {
       const int piece = pw + i * NPW;
       if (NPP * NPW > NPIECE && piece >= NPIECE) break;  // wave-uniform
-      const int e = code[i];
+      int e = code[i];
+      if constexpr (OPAQUE) asm volatile("" : "+v"(e));
       const int gy = gy0 + (e & 255), gx = gx0 + ((e >> 8) & 255);
       const bool ok = (e >> 24) && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
       const size_t off = ((size_t)(unsigned)(gy * W + gx) * CIN + (size_t)(((e >> 16) & 255) + c * HS) * 4) * 4;
@@ -1069,12 +1073,20 @@ struct GeomWS {
   static __device__ __forceinline__ int pix_off(int hy, int hx) { return hy * RPB + hx * PSB; }
 };
 
-template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP>
+// PROJ (dconv7 in front of dconv8): instead of storing the 64 channels of a pixel, the
+// epilogue parks the tile's split output in LDS (hproj, 64 px x [hi 64 | lo 64] f16, 16-B
+// chunks XOR-swizzled by pixel, in the halo buffer tile i-1 used: free until the next DMA)
+// and wave w projects pixels 16w..16w+15 onto dconv8's 25 phase taps: D[px][tap] =
+// sum_ci h[px][ci] w8[tap][ci] on the same split-f16 MFMA (2 tap blocks x 2 k32-steps x 3,
+// B fragments from an LDS copy of w8), scaled by 2^-k8 and stored tile-major (a.proj).
+// Two extra barriers per tile: hproj complete, hproj read (before the DMA overwrites it).
+template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP, bool PROJ = false>
 __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
                                         int px) {
   constexpr int NTAPS = KH * KW, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
   static_assert(TW == 8 && CIN % 32 == 0 && COUT % 16 == 0, "16-pixel tiles = two 8-pixel rows");
   static_assert(!(TRP && RESID), "no residual on the transposed phases");
+  static_assert(!PROJ || (TRP && COUT == 64 && TH * TW == 64), "projection: dconv7 8x8 tiles");
   using G = GeomWS<CIN, TH, TW>;
   using HP = HaloPieces<G, CIN, CIN, NW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
@@ -1104,6 +1116,16 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   }
   const float scale = a.wscale[model];
   const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
+  // PROJ: dconv8 B fragments (k = channel 32ks + 8g + j, column = phase tap 16nt + l16)
+  // copied to LDS once (8 KB; resident in VGPRs they would spill the main loop), published
+  // by the first tile barrier
+  constexpr int W8F = 2 * KST * 2;  // fragments per lane
+  const f16x8* w8lds = (const f16x8*)(lds + 2 * G::HALO_BYTES) + lane;
+  const float scale8 = PROJ ? a.proj_scale[model] : 0.f;
+  if constexpr (PROJ) {
+    const f16x8* src = (const f16x8*)a.proj_w + (size_t)model * W8F * 64;
+    for (int q = threadIdx.x; q < W8F * 64; q += 64 * NW) ((f16x8*)(lds + 2 * G::HALO_BYTES))[q] = src[q];
+  }
 
   // B-fragment base of each 16-pixel tile: pixel (2m + l16/8, l16%8), channels 8g..8g+7
   int boff[MT];
@@ -1123,8 +1145,8 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   auto issue = [&](int i) {
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
-    hp.issue(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4, a.zero16, a.H,
-             a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
+    hp.template issue<PROJ>(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4,
+                            a.zero16, a.H, a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
   };
 
   f32x4 acc[MT];
@@ -1167,14 +1189,58 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         f16x4 hi, lo;
         split4(v, hi, lo);
         u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
-        if (y < a.H && x < a.W) {
+        if constexpr (PROJ) {  // chunk (g & 1) * 8 + 2w + g / 2 of pixel 16m + l16
+          const int pp = 16 * m + l16, ch = (g & 1) * 8 + 2 * wave + (g >> 1);
+          *(u32x4*)(lds + ((i + 1) & 1) * G::HALO_BYTES + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
+        } else if (y < a.H && x < a.W) {
           const int oy = TRP ? 2 * y + py : y, ox = TRP ? 2 * x + px : x;
           *(u32x4*)(a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = q;
         }
       }
     }
-    if (i == ntile) break;
+    f16x8 ah[KST], al[KST];
+    if constexpr (PROJ)
+      if (i > 0) {
+        lds_reads_done();  // lgkmcnt(0): this wave's hproj writes have landed
+        stage_barrier();   // the whole tile's channels are in hproj
+        const char* hproj = lds + ((i + 1) & 1) * G::HALO_BYTES;
+        const int pp = 16 * wave + l16;
+#pragma unroll
+        for (int ks = 0; ks < KST; ++ks) {
+          ah[ks] = *(const f16x8*)(hproj + pp * 256 + (((4 * ks + g) ^ (pp & 15)) << 4));
+          al[ks] = *(const f16x8*)(hproj + pp * 256 + (((8 + 4 * ks + g) ^ (pp & 15)) << 4));
+        }
+        if (i + 1 < ntile) {
+          lds_reads_done();
+          stage_barrier();  // everyone has read hproj: the DMA may overwrite it
+        }
+      }
     if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
+    if constexpr (PROJ)
+      if (i > 0) {
+        float* dst = a.proj +
+                     ((((size_t)ep_p * 4 + 2 * py + px) * a.tiles_y + ep_y / TH) * a.tiles_x + ep_x / TW) * (25 * 64) +
+                     16 * wave + 4 * g;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          f16x8 wh[KST], wl[KST];
+#pragma unroll
+          for (int ks = 0; ks < KST; ++ks) {
+            wh[ks] = w8lds[((nt * KST + ks) * 2 + 0) * 64];
+            wl[ks] = w8lds[((nt * KST + ks) * 2 + 1) * 64];
+          }
+          f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KST; ++ks) {
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[ks], wh[ks], d, 0, 0, 0);  // a_lo*w_hi
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], wl[ks], d, 0, 0, 0);  // a_hi*w_lo
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], wh[ks], d, 0, 0, 0);  // a_hi*w_hi
+          }
+          const int tap = 16 * nt + l16;
+          if (tap < 25) *(f32x4*)(dst + tap * 64) = d * scale8;
+        }
+      }
+    if (i == ntile) break;
     tile_at(i, ep_p, ep_y, ep_x);
     if constexpr (RESID) {  // consumed by this tile's epilogue, after the next vmcnt(0)
 #pragma unroll
@@ -1619,10 +1685,10 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
 
 // Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi & 1, tap set gi >> 1
 // (the phase of a transposed layer).
-template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
+template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
 __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
   using G = GeomWS<CIN, TH, TW>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -1631,10 +1697,10 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
     ws_body<CIN, COUT, TH, TW, RESID, 3, 3, false>(a, lds, model, bi, nb, 0, 0, 0);
   } else {
     switch (gi >> 1) {  // phase-major tap bases 0, 4, 10, 16 (for_each_phase_tap)
-      case 0: ws_body<CIN, COUT, TH, TW, false, 2, 2, true>(a, lds, model, bi, nb, 0, 0, 0); break;
-      case 1: ws_body<CIN, COUT, TH, TW, false, 2, 3, true>(a, lds, model, bi, nb, 4, 0, 1); break;
-      case 2: ws_body<CIN, COUT, TH, TW, false, 3, 2, true>(a, lds, model, bi, nb, 10, 1, 0); break;
-      default: ws_body<CIN, COUT, TH, TW, false, 3, 3, true>(a, lds, model, bi, nb, 16, 1, 1); break;
+      case 0: ws_body<CIN, COUT, TH, TW, false, 2, 2, true, PROJ>(a, lds, model, bi, nb, 0, 0, 0); break;
+      case 1: ws_body<CIN, COUT, TH, TW, false, 2, 3, true, PROJ>(a, lds, model, bi, nb, 4, 0, 1); break;
+      case 2: ws_body<CIN, COUT, TH, TW, false, 3, 2, true, PROJ>(a, lds, model, bi, nb, 10, 1, 0); break;
+      default: ws_body<CIN, COUT, TH, TW, false, 3, 3, true, PROJ>(a, lds, model, bi, nb, 16, 1, 1); break;
     }
   }
 }
@@ -1778,6 +1844,40 @@ __device__ __forceinline__ void d8_load(f32x4 (&r)[D8_LOADS], const Dconv8Args& 
   }
 }
 
+// Inverse colour transform, clip and quantiser of the four output pixels (2my + py, 2mx + px)
+// of image n (decoder.py:45-48, utils.py:70-72): convert_to_rgb (Y - 0, Cb - .5, Cr - .5)
+// projected by fp32(inv kernel), clipped; 6-B stores (two pixels per output row).
+__device__ __forceinline__ void d8_store_rgb(const Dconv8Args& a, int n, int my, int mx, const float (&outv)[3][4]) {
+  const int OW = a.W * 2;
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+    uint8_t rgb[6];
+    float rgbf[6];
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      const int ph = py * 2 + px;
+      const float t0 = __fsub_rn(outv[0][ph], c_ycbcr_off[0]);
+      const float t1 = __fsub_rn(outv[1][ph], c_ycbcr_off[1]);
+      const float t2 = __fsub_rn(outv[2][ph], c_ycbcr_off[2]);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v = clip01(project(c_ycbcr_inv + 3 * c, t0, t1, t2));
+        rgbf[px * 3 + c] = v;
+        rgb[px * 3 + c] = quant255(v);
+      }
+    }
+    const size_t o = (((size_t)n * a.H * 2 + 2 * my + py) * OW + 2 * mx) * 3;
+    uint16_t* d16 = (uint16_t*)(a.out_u8 + o);  // o is even: 2-byte aligned
+    d16[0] = rgb[0] | (rgb[1] << 8);
+    d16[1] = rgb[2] | (rgb[3] << 8);
+    d16[2] = rgb[4] | (rgb[5] << 8);
+    if (a.out_f32) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HW * D8_PS];
   const int n = blockIdx.y;
@@ -1843,36 +1943,52 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 
   const int my = t0y + ty, mx = t0x + tx;
   if (my >= a.H || mx >= a.W) return;
-  const int OW = a.W * 2;
+  d8_store_rgb(a, n, my, mx, outv);
+}
+
+// ------------------------------------------------------------------------------------
+// dconv8 as a gather of dconv7's projections (f16x3 decoder tail, see ws_body PROJ):
+// output pixel (2m + (py, px)) of plane p = bias + sum over the phase's window (iy, ix) of
+// proj[m - 1 + (iy, ix)][tb(py, px) + iy (2 + px) + ix], then leaky, clip and the colour
+// epilogue.  One thread per coarse position m (8 x 32 per block), all three planes; every
+// (pixel, tap) projection feeds exactly one output, so the 25 floats per pixel are read
+// once (L2 merges the neighbouring threads' 4-B reads).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
+  const int n = blockIdx.y;
+  const int tyi = blockIdx.x / a.tiles_x;
+  const int my = tyi * D8_TH + threadIdx.x / D8_TW, mx = (blockIdx.x - tyi * a.tiles_x) * D8_TW + threadIdx.x % D8_TW;
+  if (my >= a.H || mx >= a.W) return;
+  constexpr int TB[4] = {0, 4, 10, 16};  // phase-major tap bases (for_each_phase_tap)
+  float outv[3][4];
 #pragma unroll
-  for (int py = 0; py < 2; ++py) {
-    // the two horizontally adjacent output pixels (2mx, 2mx+1) of row 2my+py: 6 bytes
-    uint8_t rgb[6];
-    float rgbf[6];
+  for (int type = 0; type < 3; ++type) {
+    const int p = type * a.nimg + n;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int px = 0; px < 2; ++px) {
-      const int ph = py * 2 + px;
-      // convert_to_rgb: (Y - 0, Cb - .5, Cr - .5) projected by fp32(inv kernel), then clip
-      const float t0 = __fsub_rn(outv[0][ph], c_ycbcr_off[0]);
-      const float t1 = __fsub_rn(outv[1][ph], c_ycbcr_off[1]);
-      const float t2 = __fsub_rn(outv[2][ph], c_ycbcr_off[2]);
+    for (int iy = 0; iy < 3; ++iy)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float v = clip01(project(c_ycbcr_inv + 3 * c, t0, t1, t2));
-        rgbf[px * 3 + c] = v;
-        rgb[px * 3 + c] = quant255(v);
+      for (int ix = 0; ix < 3; ++ix) {
+        const int ny = my - 1 + iy, nx = mx - 1 + ix;
+        const bool ok = (unsigned)ny < (unsigned)a.H && (unsigned)nx < (unsigned)a.W;
+        const int cy = ok ? ny >> 1 : 0, cx = ok ? nx >> 1 : 0, ph7 = ok ? (ny & 1) * 2 + (nx & 1) : 0;
+        const float* src =
+            a.proj + ((((size_t)p * 4 + ph7) * a.tiles_y7 + (cy >> 3)) * a.tiles_x7 + (cx >> 3)) * (25 * 64) +
+            (cy & 7) * 8 + (cx & 7);
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          const int py = ph >> 1, px = ph & 1;
+          if (iy < 2 + py && ix < 2 + px) {
+            const float v = src[(TB[ph] + iy * (2 + px) + ix) * 64];
+            acc[ph] = __fadd_rn(acc[ph], ok ? v : 0.f);
+          }
+        }
       }
-    }
-    const size_t o = (((size_t)n * a.H * 2 + 2 * my + py) * OW + 2 * mx) * 3;
-    uint16_t* d16 = (uint16_t*)(a.out_u8 + o);  // o is even: 2-byte aligned
-    d16[0] = rgb[0] | (rgb[1] << 8);
-    d16[1] = rgb[2] | (rgb[3] << 8);
-    d16[2] = rgb[4] | (rgb[5] << 8);
-    if (a.out_f32) {
+    const float b = a.bias[type > 0 ? 1 : 0];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
-    }
+    for (int ph = 0; ph < 4; ++ph) outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
   }
+  d8_store_rgb(a, n, my, mx, outv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2418,7 +2534,7 @@ static int device_cus() {
 
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
 // in proportion to each group's MFMA work (planes x taps).
-template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP>
+template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
 static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   a.tiles_y = (a.H + TH - 1) / TH;
   a.tiles_x = (a.W + TW - 1) / TW;
@@ -2434,7 +2550,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   long long work[8], total = 0;
   for (int gi = 0; gi < a.ws_ngrp; ++gi) {
     const long long planes = (gi & 1) ? a.P - a.nimg : a.nimg;
-    work[gi] = planes * per_plane * taps[gi >> 1];
+    work[gi] = planes * per_plane * (2 * taps[gi >> 1] + (PROJ ? 1 : 0));  // + projection: 12 of 24/tap MFMAs
     total += work[gi];
   }
   const int target = 2 * device_cus();
@@ -2445,8 +2561,8 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
     b = b < 1 ? 1 : b > tiles ? tiles : b;
     a.ws_blk[gi + 1] = a.ws_blk[gi] + (int)b;
   }
-  hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP>), dim3(a.ws_blk[a.ws_ngrp]), dim3(64 * (COUT / 16)),
-                     0, st, a);
+  hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP, PROJ>), dim3(a.ws_blk[a.ws_ngrp]),
+                     dim3(64 * (COUT / 16)), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2528,13 +2644,31 @@ hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// NIC_D8=tile selects the one-tile-per-block dconv8 (A/B)
-static bool use_d8_strip() {
-  static const bool on = [] {
+// dconv8 in f16x3 mode: 'p' (default) projections fused into dconv7 + gather,
+// NIC_D8=strip the strip-walk MFMA kernel, NIC_D8=tile the one-tile-per-block one (A/B)
+static char d8_mode() {
+  static const char m = [] {
     const char* e = getenv("NIC_D8");
-    return !(e && e[0] == 't');
+    return e && (e[0] == 't' || e[0] == 's') ? e[0] : 'p';
   }();
-  return on;
+  return m;
+}
+static bool use_d8_strip() { return d8_mode() != 't'; }
+
+bool dconv78_fused() { return use_ws() && d8_mode() == 'p'; }
+
+hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
+  if (!a.proj || !a.proj_w || a.OH != 2 * a.H || a.OW != 2 * a.W) return hipErrorInvalidValue;
+  return launch_ws<64, 64, 8, 8, false, true, true>(a, st);
+}
+
+hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st) {
+  if (!a.proj || (a.H & 1) || (a.W & 1)) return hipErrorInvalidValue;
+  if (a.tiles_y7 != (a.H / 2 + 7) / 8 || a.tiles_x7 != (a.W / 2 + 7) / 8) return hipErrorInvalidValue;
+  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
+  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
+  hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {

@@ -269,14 +269,17 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
 
 
-def test_alternative_kernels_parity(tmp_path):
+@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}],
+                         ids=["ws0-tile", "strip"])
+def test_alternative_kernels_parity(tmp_path, switches):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
-    NIC_D8=tile) meet the golden contract too; they run in a child process because the
-    switches are read when the library loads."""
+    NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the
+    golden contract too; they run in a child process because the switches are read when
+    the library loads."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, NIC_WS="0", NIC_D8="tile")
+    env = dict(os.environ, **switches)
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
