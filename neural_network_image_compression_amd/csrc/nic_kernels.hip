@@ -484,6 +484,10 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
 // outside the image, so a batch's loads are all in flight before the first is consumed (a
 // per-element guarded load would make the compiler wait for each load separately).
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) const char* lds_cptr_t;
+// LDS byte offset of a generic pointer into __shared__ memory, and back as an LDS pointer
+__device__ __forceinline__ unsigned lds_off(const void* p) { return (unsigned)(size_t)(lds_ptr_t)p; }
+__device__ __forceinline__ lds_cptr_t lds_at(unsigned off) { return (lds_cptr_t)(size_t)off; }
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 // One 16-B direct-to-LDS load per lane (global_load_lds_dwordx4): lane l of the wave writes
@@ -978,8 +982,9 @@ struct HaloPieces {
       const int row = q / RPS, r = q - row * RPS;
       const int sp = r / PSS, k = r - sp * PSS;
       const int hx = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
-      const bool read = q < TOTAL && sp < G::HW && k < 2 * HS;  // data slots; the rest is pad
-      const int slot = k < HS ? k : CIN / 8 + (k - HS);  // + c*HS per stage
+      // data slots (the rest is pad); swizzled records (G::SWZ) hold chunk k ^ swz(hx) in slot k
+      const bool read = q < TOTAL && sp < G::HW && (G::SWZ || k < 2 * HS);
+      const int slot = G::SWZ ? G::chunk_at(k, hx) : k < HS ? k : CIN / 8 + (k - HS);  // + c*HS per stage
       code[i] = read ? (row | hx << 8 | slot << 16 | 1 << 24) : 0;
     }
   }
@@ -1050,36 +1055,32 @@ __device__ __forceinline__ void unswap16(const u32x4& q, f16x4& hi, f16x4& lo) {
   lo = __builtin_bit_cast(f16x4, y);
 }
 
-// LDS halo image of the weight-stationary kernels (3x3 window, stride 1).  The B fragment
-// of v_mfma_f32_16x16x32_f16 has lane (g, l16) read channels 8g..8g+7 of pixel l16 = two
-// 8-pixel rows; a ds_read_b128 16-lane group then mixes (row 0, cols 0-3 | 4-7) and (row 1,
-// cols 4-7 | 0-3) of two channel chunks g, g+1.  Pixel records of 20 slots (64 B pad; 4 mod
-// 16) put columns 0..3 on slots 0, 4, 8, 12 (+ g), and a row pitch of 2 mod 4 slots moves
-// row 1 to the other two residues: all 16 lanes of a group hit distinct slots.
+// LDS halo image of the weight-stationary kernels (3x3 window, stride 1): unpadded 256-B
+// pixel records (16 slots: [hi 64 ch | lo 64 ch] in 16-B chunks), rows of HW records, and
+// chunk c of halo column hx stored in slot c ^ (2 hx mod 16).  The B fragment of
+// v_mfma_f32_16x16x32_f16 has lane (g, l16) read chunk c = 4 ks + 8 hl + g of pixel l16 (two
+// 8-pixel rows); every ds_read_b128 16-lane group ({0-3, 12-15, 20-27}, ...) then hits 16
+// distinct slots for every tap shift (exhaustive search over x-linear / XOR swizzles), and
+// the image is whole 1-KB DMA pieces with no pad slots (25 instead of 32 for 10 x 10).
 template <int CIN, int TH, int TW>
 struct GeomWS {
   static_assert(CIN == 64, "record geometry searched for Cin 64");
   static constexpr int HH = TH + 2, HW = TW + 2;
-  static constexpr bool S2 = false;
+  static constexpr bool S2 = false, SWZ = true;
   static constexpr int HE = HW;
-  static constexpr int PSB = CIN * 4 + 64;
-  static constexpr int rps() {
-    int r = HW * (PSB / 16);
-    while (r % 4 != 2) ++r;
-    return r;
-  }
-  static constexpr int RPB = rps() * 16;
-  static constexpr int HALO_BYTES = (HH * RPB + 1023) / 1024 * 1024;
-  static __device__ __forceinline__ int pix_off(int hy, int hx) { return hy * RPB + hx * PSB; }
+  static constexpr int PSB = CIN * 4;
+  static constexpr int RPB = HW * PSB;
+  static constexpr int HALO_BYTES = HH * RPB;
+  static_assert(HALO_BYTES % 1024 == 0, "whole DMA pieces");
+  static __device__ __forceinline__ int chunk_at(int slot, int hx) { return slot ^ ((2 * hx) & 15); }
 };
 
 // PROJ (dconv7 in front of dconv8): instead of storing the 64 channels of a pixel, the
 // epilogue parks the tile's split output in LDS (hproj, 64 px x [hi 64 | lo 64] f16, 16-B
-// chunks XOR-swizzled by pixel, in the halo buffer tile i-1 used: free until the next DMA)
-// and wave w projects pixels 16w..16w+15 onto dconv8's 25 phase taps: D[px][tap] =
+// chunks XOR-swizzled by pixel) and wave w projects pixels 16w..16w+15 onto dconv8's 25 phase taps: D[px][tap] =
 // sum_ci h[px][ci] w8[tap][ci] on the same split-f16 MFMA (2 tap blocks x 2 k32-steps x 3,
 // B fragments from an LDS copy of w8), scaled by 2^-k8 and stored tile-major (a.proj).
-// Two extra barriers per tile: hproj complete, hproj read (before the DMA overwrites it).
+// One extra barrier per tile (hproj complete); the next tile's barrier orders its reuse.
 template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP, bool PROJ = false>
 __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
                                         int px) {
@@ -1122,15 +1123,21 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   constexpr int W8F = 2 * KST * 2;  // fragments per lane
   const f16x8* w8lds = (const f16x8*)(lds + 2 * G::HALO_BYTES) + lane;
   const float scale8 = PROJ ? a.proj_scale[model] : 0.f;
+  char* hproj = lds + 2 * G::HALO_BYTES + W8F * 64 * 16;
   if constexpr (PROJ) {
     const f16x8* src = (const f16x8*)a.proj_w + (size_t)model * W8F * 64;
     for (int q = threadIdx.x; q < W8F * 64; q += 64 * NW) ((f16x8*)(lds + 2 * G::HALO_BYTES))[q] = src[q];
   }
 
-  // B-fragment base of each 16-pixel tile: pixel (2m + l16/8, l16%8), channels 8g..8g+7
-  int boff[MT];
+  // B fragments: pixel (2m + l16/8 + kh, l16%8 + kw), chunk c = 8 hl + 4 ks + g in slot
+  // c ^ swz(l16%8 + kw).  bx[kw] = record address (m = kh = 0) | slot of chunk g; chunk
+  // 8 hl + 4 ks then XORs bits 6..7, and (2m + kh) rows add an immediate offset.
+  int bx[KW];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) boff[m] = G::pix_off(2 * m + (l16 >> 3), l16 & 7) + g * 16;
+  for (int kw = 0; kw < KW; ++kw) {
+    const int hx = (l16 & 7) + kw;
+    bx[kw] = (l16 >> 3) * G::RPB + hx * G::PSB + (G::chunk_at(g, hx) << 4);
+  }
 
   HP hp;
   hp.init(wave, lane);
@@ -1145,7 +1152,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   auto issue = [&](int i) {
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
-    hp.template issue<PROJ>(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4,
+    hp.template issue<true>(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4,
                             a.zero16, a.H, a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
   };
 
@@ -1191,7 +1198,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
         if constexpr (PROJ) {  // chunk (g & 1) * 8 + 2w + g / 2 of pixel 16m + l16
           const int pp = 16 * m + l16, ch = (g & 1) * 8 + 2 * wave + (g >> 1);
-          *(u32x4*)(lds + ((i + 1) & 1) * G::HALO_BYTES + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
+          *(u32x4*)(hproj + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
         } else if (y < a.H && x < a.W) {
           const int oy = TRP ? 2 * y + py : y, ox = TRP ? 2 * x + px : x;
           *(u32x4*)(a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = q;
@@ -1203,16 +1210,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
       if (i > 0) {
         lds_reads_done();  // lgkmcnt(0): this wave's hproj writes have landed
         stage_barrier();   // the whole tile's channels are in hproj
-        const char* hproj = lds + ((i + 1) & 1) * G::HALO_BYTES;
         const int pp = 16 * wave + l16;
 #pragma unroll
         for (int ks = 0; ks < KST; ++ks) {
           ah[ks] = *(const f16x8*)(hproj + pp * 256 + (((4 * ks + g) ^ (pp & 15)) << 4));
           al[ks] = *(const f16x8*)(hproj + pp * 256 + (((8 + 4 * ks + g) ^ (pp & 15)) << 4));
-        }
-        if (i + 1 < ntile) {
-          lds_reads_done();
-          stage_barrier();  // everyone has read hproj: the DMA may overwrite it
         }
       }
     if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
@@ -1256,33 +1258,39 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #endif
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // bx in this buffer (HALO_BYTES is a multiple of 256: the XOR bits are untouched)
+    unsigned bb[KW];
+#pragma unroll
+    for (int kw = 0; kw < KW; ++kw) bb[kw] = lds_off(buf) + bx[kw];
     // NTAPS x KST k32-steps, fully unrolled (the weight registers are indexed statically).
     // Rolling fragment buffer: once pixel tile m's three MFMAs of step s are issued, its
     // registers receive step s+1's fragment, (MT-1)*3 MFMAs before they are needed.
     constexpr int NSTEP = NTAPS * KST;
     f16x8 fb[MT][2];
-    auto step_off = [&](int st) {
+    // fragment (hi or lo) of pixel tile m at step st: chunk variant 2 hl + ks (bits 6..7 =
+    // 8 hl + 4 ks), row 2m + kh
+    auto frag = [&](int m, int st, int hl) {
       const int t = st / KST, ks = st - t * KST, kh = t / KW, kw = t - kh * KW;
-      return kh * G::RPB + kw * G::PSB + ks * 64;
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(bb[kw] ^ ((2 * hl + ks) << 6)) +
+                                                               (2 * m + kh) * G::RPB);
     };
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      fb[m][0] = *(const f16x8*)(buf + boff[m] + step_off(0));
-      fb[m][1] = *(const f16x8*)(buf + boff[m] + step_off(0) + CIN * 2);
+      fb[m][0] = frag(m, 0, 0);
+      fb[m][1] = frag(m, 0, 1);
     }
     __builtin_amdgcn_s_setprio(1);  // the MFMA stream outranks the partner wave's epilogue / DMA issue
 #pragma unroll
     for (int st = 0; st < NSTEP; ++st) {
       const int t = st / KST, ks = st - t * KST;
-      const int noff = step_off(st + 1 < NSTEP ? st + 1 : st);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
         if (st + 1 < NSTEP) {
-          fb[m][0] = *(const f16x8*)(buf + boff[m] + noff);
-          fb[m][1] = *(const f16x8*)(buf + boff[m] + noff + CIN * 2);
+          fb[m][0] = frag(m, st + 1, 0);
+          fb[m][1] = frag(m, st + 1, 1);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
       }
@@ -1688,7 +1696,8 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
 __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
   using G = GeomWS<CIN, TH, TW>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 : 0)];
+  __shared__ __attribute__((aligned(16)))
+  char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 + TH * TW * COUT * 4 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -1950,14 +1959,19 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 // dconv8 as a gather of dconv7's projections (f16x3 decoder tail, see ws_body PROJ):
 // output pixel (2m + (py, px)) of plane p = bias + sum over the phase's window (iy, ix) of
 // proj[m - 1 + (iy, ix)][tb(py, px) + iy (2 + px) + ix], then leaky, clip and the colour
-// epilogue.  One thread per coarse position m (8 x 32 per block), all three planes; every
-// (pixel, tap) projection feeds exactly one output, so the 25 floats per pixel are read
-// once (L2 merges the neighbouring threads' 4-B reads).
+// epilogue.  One thread per coarse position m, all three planes; every (pixel, tap)
+// projection feeds exactly one output, so the 25 floats per pixel are read once.  Block =
+// 16 x 16 positions; wave w takes the positions of parity (w / 2, w % 2), 8 x 8 at stride
+// 2, so for every (iy, ix) its 64 neighbours share one dconv7 phase and form an 8 x 8
+// window of that phase's coarse grid: each load reads whole 32-B rows of the tile-major
+// projection planes.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
   const int n = blockIdx.y;
   const int tyi = blockIdx.x / a.tiles_x;
-  const int my = tyi * D8_TH + threadIdx.x / D8_TW, mx = (blockIdx.x - tyi * a.tiles_x) * D8_TW + threadIdx.x % D8_TW;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int my = tyi * 16 + 2 * (lane >> 3) + (wave >> 1);
+  const int mx = (blockIdx.x - tyi * a.tiles_x) * 16 + 2 * (lane & 7) + (wave & 1);
   if (my >= a.H || mx >= a.W) return;
   constexpr int TB[4] = {0, 4, 10, 16};  // phase-major tap bases (for_each_phase_tap)
   float outv[3][4];
@@ -2665,8 +2679,8 @@ hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
 hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st) {
   if (!a.proj || (a.H & 1) || (a.W & 1)) return hipErrorInvalidValue;
   if (a.tiles_y7 != (a.H / 2 + 7) / 8 || a.tiles_x7 != (a.W / 2 + 7) / 8) return hipErrorInvalidValue;
-  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
-  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
+  const int tiles_y = (a.H + 15) / 16;
+  a.tiles_x = (a.W + 15) / 16;
   hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
