@@ -22,8 +22,8 @@ LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first ma
     (r"conv_ws2_kernel<32, 64", "conv2"), (r"conv_ws2_kernel<64, 32", "conv8"),
     (r"<32, 64, 5, 2, false", "conv2"), (r"<64, 32, 5, 2, false", "conv8"),
     (r"<32, 64, 5, 2, true", "dconv1"), (r"<64, 64, 5, 2, true", "dconv7"),
-    (r"conv_ws_kernel<64, 64, 8, 8, false, true>", "dconv7"),
-    (r"conv_ws_kernel<64, 64, 8, 8, true, false>", "k3_resid"), (r"conv_ws_kernel<64, 64, 8, 8, false, false>", "k3"),
+    (r"dconv8_gather", "dconv8"), (r"conv_ws_kernel<64, 64, 8, 8, false, true", "dconv7"),
+    (r"conv_ws_kernel<64, 64, 8, 8, true, false", "k3_resid"), (r"conv_ws_kernel<64, 64, 8, 8, false, false", "k3"),
     (r"<64, 64, 3, 1, false.*true>", "k3_resid"), (r"<64, 64, 3, 1, false.*false>", "k3"),
     (r"latent_hist", "hist"), (r"hist_entropy", "entropy"),
 ]
