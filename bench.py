@@ -194,6 +194,16 @@ def main():
     lt = codec.layer_times()
     codec.set_timing(False)
     torch.cuda.synchronize()
+    ent_ms = None
+    if args.workload == "4k":
+        # histogram entropy: torch events on the current stream (the one nic_entropy_hist runs on)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            codec.entropy(z)
+        e1.record()
+        torch.cuda.synchronize()
+        ent_ms = e0.elapsed_time(e1) / args.steps
 
     if rank != 0:
         barrier()
@@ -232,6 +242,12 @@ def main():
             layers[name]["fused"] = "conv1 (colour transform + conv1 computed into conv2's LDS halo)"
         if name == "dconv7" and d78_fused:
             layers[name]["fused"] = "dconv8's MACs (25 tap projections per output pixel, split-f16 MFMA)"
+    if ent_ms is not None:
+        nbytes = B * h8 * w8 * 96 + 3 * B * 4  # u8 latent read once + 3 floats per image
+        layers["entropy"] = {"avg_ms": round(ent_ms, 4), "gbytes_per_launch": round(nbytes / 1e9, 4),
+                             "gbps": round(nbytes / (ent_ms * 1e-3) / 1e9, 1),
+                             "hbm_frac": round(nbytes / (ent_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "kernels": "latent_hist_kernel (per-block partial counts) + hist_entropy_kernel (reduce + entropy)"}
     dom = max((k for k in layers if "tflops" in layers[k]), key=lambda k: layers[k]["avg_ms"])
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -249,7 +265,8 @@ def main():
                 "flop_per_launch": flops[dom], "avg_launch_ms": layers[dom]["avg_ms"],
                 "peak_basis": ("dense f16 MFMA 2.5 PFLOP/s / 3 passes (algorithmic fp32 FLOP)"
                                if args.precision == "f16x3" else "dense fp32 MFMA 157.3 TFLOP/s")}
-    total_flop = sum(geo.values()) * P  # every layer runs once per step (conv1 possibly fused)
+    enc_only = args.workload == "4k"
+    total_flop = sum(v for k, v in geo.items() if not (enc_only and k.startswith("dconv"))) * P
     ms_step = el / args.steps * 1e3
     value = world * B * H * W * args.steps / 1e6 / el
     out = {

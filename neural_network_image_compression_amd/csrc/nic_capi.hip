@@ -584,7 +584,7 @@ int nic_reserve(nic_ctx* c, int n, int h, int w) {
   float* R[4];
   int rc = ensure_regions(c, std::max(e.r0, d.r0), std::max(e.r123, d.r123), R);
   if (rc) return rc;
-  const size_t cb = (size_t)3 * n * 256 * sizeof(uint32_t);
+  const size_t cb = n > 0 ? hist_scratch_bytes(n, e.c8y.out * e.c8x.out) : 0;
   if (cb > c->counts_bytes) {
     if (c->counts) HIP_TRY(hipFree(c->counts));
     c->counts = nullptr;
@@ -768,20 +768,17 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
   if (n == 0 || (!counts && !bits)) return NIC_OK;
   if (!latent) return fail(NIC_EINVAL, "nic_entropy_hist: NULL latent");
   if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_entropy_hist: batch %d too large", n);
+  if ((long long)h8 * w8 * 6 > 0x7fffffffLL) return fail(NIC_ESHAPE, "nic_entropy_hist: latent %dx%d too large", h8, w8);
   DeviceGuard guard(c->device);
-  uint32_t* cnt = counts;
-  if (!cnt) {
-    const size_t cb = (size_t)3 * n * 256 * sizeof(uint32_t);
-    if (cb > c->counts_bytes) {
-      if (c->counts) HIP_TRY(hipFree(c->counts));
-      c->counts = nullptr;
-      c->counts_bytes = 0;
-      HIP_TRY(hipMalloc(&c->counts, cb));
-      c->counts_bytes = cb;
-    }
-    cnt = c->counts;
+  const size_t cb = hist_scratch_bytes(n, h8 * w8);
+  if (cb > c->counts_bytes) {
+    if (c->counts) HIP_TRY(hipFree(c->counts));
+    c->counts = nullptr;
+    c->counts_bytes = 0;
+    HIP_TRY(hipMalloc(&c->counts, cb));
+    c->counts_bytes = cb;
   }
-  HIP_TRY(launch_hist(latent, n, h8 * w8, cnt, bits, (hipStream_t)stream));
+  HIP_TRY(launch_hist(latent, n, h8 * w8, c->counts, counts, bits, (hipStream_t)stream));
   return NIC_OK;
 }
 

@@ -94,7 +94,11 @@ hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st);   // split-f16 MFMA
 bool dconv78_fused();
 hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st);
 hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st);
-hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st);
+// histogram entropy: per-block partial counts into `part` (hist_scratch_bytes), then one
+// reduce kernel writes counts (optional) and bits/symbol (optional)
+size_t hist_scratch_bytes(int nimg, int plane_px);
+hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
+                       hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 
 }  // namespace nic

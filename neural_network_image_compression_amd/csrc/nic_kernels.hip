@@ -2389,49 +2389,109 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
 // Histogram entropy (tf1_13/src/training.py:66-71) and bitstream pack/unpack
 // (utils.py:35-40).
 // ------------------------------------------------------------------------------------
+// One block reads a contiguous byte range of one image's latent (h, w, 96) with 16-B loads
+// (every pixel = 6 vectors: vectors 0-1 Y, 2-3 Cb, 4-5 Cr) and counts all three planes
+// into LDS histograms replicated R times, replica-minor ([plane][bin][r], r = lane % R),
+// so lanes that hit the same bin (skewed latents: ~40 % zeros) spread over R banks.  Each
+// block writes its 3 x 256 partial counts (no atomics, no memset); hist_entropy_kernel
+// reduces them.  HBM-bound: 1 B read per code.
+constexpr int HIST_UNR = 4;  // 16-B loads in flight per thread
+template <int R, bool ZB>
 __global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restrict__ z, int nimg, int plane_px,
-                                                          uint32_t* __restrict__ counts, int chunk_px) {
-  // grid: (chunks, 3N).  Block counts codes of plane p (= type*N + n) over pixels
-  // [chunk*chunk_px, ...) into an LDS histogram, then one atomic per non-empty bin.
-  __shared__ uint32_t h[256];
-  const int p = blockIdx.y;
-  const int n = p % nimg, type = p / nimg;
-  h[threadIdx.x] = 0;
+                                                          uint32_t* __restrict__ counts, int chunk_vec) {
+  __shared__ uint32_t h[3 * 256 * R];
+  for (int i = threadIdx.x; i < 3 * 256 * R; i += 256) h[i] = 0;
   __syncthreads();
-  const uint8_t* base = z + (size_t)n * plane_px * 96 + type * 32;
-  const int px0 = blockIdx.x * chunk_px;
-  const int px1 = min(px0 + chunk_px, plane_px);
-  // each pixel holds 32 contiguous codes = 2 x 16 B
-  for (int idx = px0 * 2 + threadIdx.x; idx < px1 * 2; idx += 256) {
-    const int px = idx >> 1, part = idx & 1;
-    const uint4 v = *(const uint4*)(base + (size_t)px * 96 + part * 16);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const int n = blockIdx.y;
+  const int nvec = plane_px * 6;
+  const u32x4* __restrict__ base = (const u32x4*)(z + (size_t)n * plane_px * 96);
+  const int v0 = blockIdx.x * chunk_vec;
+  const int v1 = min(v0 + chunk_vec, nvec);
+  const int lane = threadIdx.x & 63;
+  uint32_t* hr = h + (threadIdx.x & (R - 1));
+  uint32_t zeros[3] = {0, 0, 0};  // ZB: per-lane count of code 0, per plane
+  for (int v = v0 + threadIdx.x; v < v1; v += 256 * HIST_UNR) {
+    u32x4 q[HIST_UNR];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      atomicAdd(&h[w[k] & 255], 1u);
-      atomicAdd(&h[(w[k] >> 8) & 255], 1u);
-      atomicAdd(&h[(w[k] >> 16) & 255], 1u);
-      atomicAdd(&h[w[k] >> 24], 1u);
+    for (int u = 0; u < HIST_UNR; ++u)
+      q[u] = v + u * 256 < v1 ? __builtin_nontemporal_load(base + v + u * 256) : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < HIST_UNR; ++u) {
+      if (v + u * 256 >= v1) break;
+      const int plane = ((v + u * 256) % 6) >> 1;
+      uint32_t* hp = hr + plane * (256 * R);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = q[u][k];
+#pragma unroll
+        for (int by = 0; by < 4; ++by) {
+          const uint32_t b = (w >> (8 * by)) & 255;
+          if (ZB) {
+            if (b == 0) {
+              zeros[0] += plane == 0;
+              zeros[1] += plane == 1;
+              zeros[2] += plane == 2;
+            } else {
+              atomicAdd(&hp[b * R], 1u);
+            }
+          } else {
+            atomicAdd(&hp[b * R], 1u);
+          }
+        }
+      }
+    }
+  }
+  if (ZB) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      uint32_t c = zeros[pl];
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      if (lane == 0 && c) atomicAdd(&h[pl * 256 * R], c);
     }
   }
   __syncthreads();
-  const uint32_t c = h[threadIdx.x];
-  if (c) atomicAdd(&counts[(size_t)p * 256 + threadIdx.x], c);
+  // partial counts of this block: part[type][n][chunk][bin] (reduced by hist_entropy_kernel)
+  for (int i = threadIdx.x; i < 3 * 256; i += 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) c += h[i * R + r];
+    const int type = i >> 8, bin = i & 255;
+    counts[(((size_t)type * nimg + n) * gridDim.x + blockIdx.x) * 256 + bin] = c;
+  }
 }
 
-__global__ __launch_bounds__(256) void hist_entropy_kernel(const uint32_t* __restrict__ counts, float n_sym,
-                                                           float* __restrict__ bits) {
-  // one block per plane: p_i = c_i / N (fp32), term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2)
-  __shared__ double part[4];
+__global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __restrict__ part, int chunks, float n_sym,
+                                                            uint32_t* __restrict__ counts, float* __restrict__ bits) {
+  // one block per plane p; thread (g, bin) sums every 4th partial of the plane (exact
+  // integers, 8 loads in flight), the 4 groups meet in LDS.  Then p_i = c_i / N (fp32),
+  // term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2), summed in double.
+  __shared__ uint32_t grp[3][256];
+  __shared__ double red[4];
   const int p = blockIdx.x;
-  const float pr = __fdiv_rn((float)counts[(size_t)p * 256 + threadIdx.x], n_sym);
-  const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
-  const float term = __fmul_rn(pr, __fdiv_rn(-lg, 0.693147182464599609375f));
-  double s = (double)term;
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  const int bin = threadIdx.x & 255, g = threadIdx.x >> 8;
+  const uint32_t* src = part + (size_t)p * chunks * 256 + bin;
+  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int k = g;
+  for (; k + 28 < chunks; k += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += src[(size_t)(k + 4 * u) * 256];
+  }
+  for (; k < chunks; k += 4) acc[0] += src[(size_t)k * 256];
+  uint32_t c = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (g) grp[g - 1][bin] = c;
   __syncthreads();
-  if (threadIdx.x == 0) bits[p] = (float)(((part[0] + part[1]) + part[2]) + part[3]);
+  double s = 0.0;
+  if (g == 0) {
+    c += grp[0][bin] + grp[1][bin] + grp[2][bin];
+    if (counts) counts[(size_t)p * 256 + bin] = c;
+    const float pr = __fdiv_rn((float)c, n_sym);
+    const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
+    s = (double)__fmul_rn(pr, __fdiv_rn(-lg, 0.693147182464599609375f));
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((bin & 63) == 0) red[bin >> 6] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && bits) bits[p] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
 }
 
 __global__ __launch_bounds__(256) void pack_latent_kernel(const uint8_t* __restrict__ z, uint8_t* __restrict__ out,
@@ -2705,19 +2765,39 @@ hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* counts, float* bits, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(counts, 0, (size_t)3 * nimg * 256 * sizeof(uint32_t), st);
+int hist_chunks(int nimg, int plane_px, int* chunk_vec) {
+  // ~1536 blocks over the whole batch (6 resident per CU x 256 CUs: one full wave of
+  // blocks, no tail round), 4 KB .. 256 KB of latent each
+  const long long nvec = (long long)plane_px * 6;
+  long long cv = ((nvec * nimg + 1535) / 1536 + 255) / 256 * 256;
+  cv = cv < 256 ? 256 : (cv > 16384 ? 16384 : cv);
+  *chunk_vec = (int)cv;
+  return (int)((nvec + cv - 1) / cv);
+}
+
+size_t hist_scratch_bytes(int nimg, int plane_px) {
+  int cv;
+  return (size_t)3 * nimg * hist_chunks(nimg, plane_px, &cv) * 256 * sizeof(uint32_t);
+}
+
+hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
+                       hipStream_t st) {
+  int chunk_vec;
+  const int chunks = hist_chunks(nimg, plane_px, &chunk_vec);
+  const char* hv = getenv("NIC_HIST");
+  const char m = hv ? hv[0] : '8';  // A/B switch (tools/hist_ab.py); 8 replicas measured best
+  const bool zb = hv && hv[1] == 'z';
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(256), 0, st, z, nimg, plane_px, part, chunk_vec);
+  };
+  if (m == '1') zb ? go(latent_hist_kernel<1, true>) : go(latent_hist_kernel<1, false>);
+  else if (m == '8') zb ? go(latent_hist_kernel<8, true>) : go(latent_hist_kernel<8, false>);
+  else zb ? go(latent_hist_kernel<4, true>) : go(latent_hist_kernel<4, false>);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int chunk_px = 1024;
-  const int chunks = (plane_px + chunk_px - 1) / chunk_px;
-  hipLaunchKernelGGL(latent_hist_kernel, dim3(chunks, 3 * nimg), dim3(256), 0, st, z, nimg, plane_px, counts,
-                     chunk_px);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (bits) {
-    hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(256), 0, st, counts, (float)plane_px * 32.0f, bits);
-    e = hipGetLastError();
-  }
-  return e;
+  hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, chunks, (float)plane_px * 32.0f,
+                     counts, bits);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack(const uint8_t* z, uint8_t* out, int nimg, int h8, int w8, bool unpack, hipStream_t st) {
