@@ -96,8 +96,14 @@ def parity_sample(codec, x0, weights):
     r = codec.decode(z).cpu().numpy()
     torch.cuda.synchronize()
     r_ref = O.decode(weights, O.encode(weights, xh))
-    return {"psnr_gpu_vs_oracle_db": round(O.psnr(r, r_ref), 2),
-            "psnr_x_gpu_db": round(O.psnr(xh, r), 4), "psnr_x_oracle_db": round(O.psnr(xh, r_ref), 4)}
+    out = {"psnr_gpu_vs_oracle_db": round(O.psnr(r, r_ref), 2),
+           "psnr_x_gpu_db": round(O.psnr(xh, r), 4), "psnr_x_oracle_db": round(O.psnr(xh, r_ref), 4)}
+    if min(xh.shape[1:3]) >= 176:
+        # MS-SSIM (calc_ssim.py:13) of the GPU reconstruction by the GPU metric, and of the
+        # oracle's reconstruction by the oracle's metric
+        out["msssim_x_gpu"] = round(float(codec.ms_ssim(x0, torch.from_numpy(r).to(x0.device)).item()), 6)
+        out["msssim_x_oracle"] = round(float(O.ms_ssim(xh, r_ref)[0]), 6)
+    return out
 
 
 def main():
@@ -204,6 +210,25 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ent_ms = e0.elapsed_time(e1) / args.steps
+    quality = None
+    if args.workload in ("config2", "kodak") and min(H, W) >= 176:
+        # device MS-SSIM (nic_ms_ssim) and PSNR (nic_sq_err) of the batch's reconstruction;
+        # outside the encode+decode metric, timed with torch events on the current stream
+        rec = codec.decode(codec.encode(x))
+        codec.ms_ssim(x, rec)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            ms = codec.ms_ssim(x, rec)
+        e1.record()
+        torch.cuda.synchronize()
+        q_ms = e0.elapsed_time(e1) / args.steps
+        nbytes = 2 * B * H * W * 3  # both u8 images read once at scale 0
+        quality = {"ms_ssim_mean": round(float(ms.mean().item()), 6), "psnr_db": round(codec.psnr(x, rec), 4),
+                   "ms_ssim_ms": round(q_ms, 4), "ms_ssim_mp_per_s": round(B * H * W / 1e6 / (q_ms * 1e-3), 1),
+                   "ms_ssim_gbps_scale0": round(nbytes / (q_ms * 1e-3) / 1e9, 1),
+                   "kernels": "ssim_tile_kernel x5 scales + ssim_pool_kernel x4 + msssim_combine_kernel"}
 
     if rank != 0:
         barrier()
@@ -284,6 +309,8 @@ def main():
         "step_frac_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / peak, 4),
         "roofline": roofline, "layers": layers,
     }
+    if quality is not None:
+        out["quality"] = quality
     if args.workload == "4k":
         out["metric"] = "Megapixels/sec encode + entropy (4K frames)"
         out["frames_per_s"] = round(world * B * args.steps / el, 2)

@@ -14,6 +14,9 @@
  *   ProClass._feed_batch pack/unpack            nic_pack_latent / nic_unpack_latent
  *     utils.py:35-36, 39-40
  *   disc_entropy tf1_13/src/training.py:66-71   nic_entropy_hist
+ *   tf.image.ssim_multiscale(x1, x2, 255)       nic_ms_ssim
+ *     tf2_0/tests/calc_ssim.py:13
+ *   PSNR (the benchmark's quality figure)       nic_sq_err
  *
  * Conventions
  *  - Every buffer argument is a DEVICE pointer owned by the caller (e.g. a torch-ROCm
@@ -122,6 +125,19 @@ int nic_decode(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint8
  * bits/symbol.  Needs a ctx only for its scratch. */
 int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,
                      void* stream);
+
+/* MS-SSIM of tf.image.ssim_multiscale(a, b, max_val=255) (tf2_0/tests/calc_ssim.py:13)
+ * per image: a, b u8 (n,h,w,3) -> ms_ssim (n,) fp32.  TF defaults: 11-tap Gaussian
+ * (sigma 1.5), k1 0.01, k2 0.03, power factors (0.0448, 0.2856, 0.3001, 0.2363, 0.1333),
+ * SYMMETRIC-padded 2x2 average pooling between scales; h, w >= 176.
+ * per_scale (nullable): (n,3,5,2) fp32 mean SSIM and mean cs per channel and scale.
+ * fp32 filtering, fp64 reductions.  Needs a ctx only for its scratch. */
+int nic_ms_ssim(nic_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int h, int w, float* ms_ssim,
+                float* per_scale, void* stream);
+
+/* Exact per-image sum of squared differences of two u8 tensors of n images of
+ * bytes_per_image bytes: sse (n,) uint64.  PSNR = 10 log10(255^2 * bytes / sse). */
+int nic_sq_err(const uint8_t* a, const uint8_t* b, int n, int64_t bytes_per_image, uint64_t* sse, void* stream);
 
 /* Bitstream image layout of ProClass._feed_batch: (n,h8,w8,96) <-> (n,4*h8,8*w8,3), each
  * plane a raw C-order reshape (utils.py:35-36, 39-40). */

@@ -57,6 +57,8 @@ _SIGNATURES = {
     "nic_get_precision": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),
     "nic_set_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_layer_times": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "nic_ms_ssim": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "nic_sq_err": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int64, c_vp, c_vp]),
     "nic_pack_latent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
     "nic_unpack_latent": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
 }

@@ -169,6 +169,54 @@ class Codec:
         _lib.check(rc, "nic_entropy_hist")
         return (bits, cnt) if counts else bits
 
+    def ms_ssim(self, a, b, per_scale: bool = False):
+        """tf.image.ssim_multiscale(a, b, max_val=255) per image (calc_ssim.py:13): (N,) fp32
+        [, (N,3,5,2) mean SSIM / mean cs per channel and scale]."""
+        torch = _torch()
+        a = self._check_dev(a, 4, 3, "ms_ssim")
+        b = self._check_dev(b, 4, 3, "ms_ssim")
+        if a.shape != b.shape:
+            raise ValueError(f"ms_ssim: shapes differ {tuple(a.shape)} vs {tuple(b.shape)}")
+        n, h, w, _ = a.shape
+        out = torch.empty((n,), dtype=torch.float32, device=a.device)
+        ps = torch.empty((n, 3, 5, 2), dtype=torch.float32, device=a.device) if per_scale else None
+        rc = self._L.nic_ms_ssim(self._h, a.data_ptr(), b.data_ptr(), n, h, w, out.data_ptr(),
+                                 ps.data_ptr() if ps is not None else None, _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_ms_ssim")
+        return (out, ps) if per_scale else out
+
+    def sq_err(self, a, b):
+        """Exact per-image sum of squared differences of two u8 tensors (N,...): (N,) int64."""
+        torch = _torch()
+        for t in (a, b):
+            if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or t.device.type != "cuda":
+                raise TypeError("sq_err: expected cuda torch.uint8 tensors")
+        if a.shape != b.shape or a.ndim < 1:
+            raise ValueError(f"sq_err: shapes differ {tuple(a.shape)} vs {tuple(b.shape)}")
+        a, b = a.contiguous(), b.contiguous()
+        n = a.shape[0]
+        out = torch.empty((n,), dtype=torch.int64, device=a.device)
+        per = a.numel() // n if n else 0
+        _lib.check(self._L.nic_sq_err(a.data_ptr(), b.data_ptr(), n, per, out.data_ptr(),
+                                      _stream_ptr(torch, self.device)), "nic_sq_err")
+        return out
+
+    def psnr(self, a, b, max_val: float = 255.0, per_image: bool = False):
+        """PSNR in dB over the whole batch (as the oracle's psnr) or per image, from the exact
+        device sum of squared errors."""
+        import math
+
+        sse = self.sq_err(a, b).cpu().numpy().astype(np.float64)
+        n = a.shape[0]
+        per = a.numel() // n if n else 0
+
+        def db(s, count):
+            return float("inf") if s == 0 else 10.0 * math.log10(max_val ** 2 * count / s)
+
+        if per_image:
+            return np.array([db(s, per) for s in sse])
+        return db(float(sse.sum()), per * n)
+
     def pack(self, z):
         """(N,h,w,96) -> (N,4h,8w,3) bitstream image (utils.py:39-40)."""
         torch = _torch()

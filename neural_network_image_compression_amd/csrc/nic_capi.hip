@@ -268,6 +268,8 @@ struct nic_ctx {
   size_t ws_bytes = 0;
   uint32_t* counts = nullptr;
   size_t counts_bytes = 0;
+  char* qs = nullptr;  // MS-SSIM scratch (pooled scales + tile sums), grown on demand
+  size_t qs_bytes = 0;
   // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
   // call, read back and accumulated by nic_layer_times
   bool timing = false;
@@ -420,7 +422,7 @@ bool models_ready(const nic_ctx* c, int m0) {
 
 extern "C" {
 
-int nic_version(void) { return 100; }
+int nic_version(void) { return 200; }
 
 int nic_constants(float* ycbcr9, float* ycbcr_inv9, float* off3) {
   // host copy of what nic_create uploads; lets tests compare with np.linalg.inv (utils.py:8)
@@ -488,6 +490,7 @@ int nic_create(int device, nic_ctx** out) {
   float kf[9], kinv[9], off[3];
   nic_constants(kf, kinv, off);
   hipError_t e = upload_constants(lut, kf, kinv, off);
+  if (e == hipSuccess) e = upload_ssim_constants();
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     nic_destroy(c);
@@ -507,6 +510,7 @@ int nic_destroy(nic_ctx* c) {
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
+  if (c->qs) (void)hipFree(c->qs);
   if (c->zero16) (void)hipFree(c->zero16);
   if (c->wproj) (void)hipFree(c->wproj);
   for (int i = 0; i < L_COUNT; ++i)
@@ -779,6 +783,42 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
     c->counts_bytes = cb;
   }
   HIP_TRY(launch_hist(latent, n, h8 * w8, c->counts, counts, bits, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_ms_ssim(nic_ctx* c, const uint8_t* a, const uint8_t* b, int n, int h, int w, float* ms_ssim,
+                float* per_scale, void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_ms_ssim: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_ms_ssim: bad image shape (%d,%d,%d,3)", n, h, w);
+  if (h < 176 || w < 176)
+    return fail(NIC_ESHAPE, "nic_ms_ssim: images must be at least 176x176 (5 scales of an 11x11 window), got %dx%d",
+                h, w);
+  if (n == 0) return NIC_OK;
+  if (!a || !b || !ms_ssim) return fail(NIC_EINVAL, "nic_ms_ssim: NULL argument");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_ms_ssim: batch %d too large", n);
+  DeviceGuard guard(c->device);
+  SsimPlan pl;
+  ssim_plan(n, h, w, &pl);
+  if (pl.bytes > c->qs_bytes) {
+    if (c->qs) HIP_TRY(hipFree(c->qs));
+    c->qs = nullptr;
+    c->qs_bytes = 0;
+    if (hipMalloc(&c->qs, pl.bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(NIC_ENOMEM, "nic_ms_ssim: scratch allocation of %zu bytes failed", pl.bytes);
+    }
+    c->qs_bytes = pl.bytes;
+  }
+  HIP_TRY(launch_ms_ssim(a, b, n, h, w, c->qs, ms_ssim, per_scale, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_sq_err(const uint8_t* a, const uint8_t* b, int n, int64_t bytes_per_image, uint64_t* sse, void* stream) {
+  if (n < 0 || bytes_per_image < 0) return fail(NIC_ESHAPE, "nic_sq_err: bad shape (%d, %lld)", n, (long long)bytes_per_image);
+  if (n == 0) return NIC_OK;
+  if (!a || !b || !sse) return fail(NIC_EINVAL, "nic_sq_err: NULL argument");
+  if (n > 65535) return fail(NIC_ESHAPE, "nic_sq_err: batch %d too large", n);
+  HIP_TRY(launch_sq_err(a, b, n, bytes_per_image, reinterpret_cast<unsigned long long*>(sse), (hipStream_t)stream));
   return NIC_OK;
 }
 

@@ -101,4 +101,40 @@ hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part,
                        hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 
+// --- quality metrics (nic_quality.hip) ---------------------------------------------------
+constexpr int kSsimScales = 5;  // tf.image.ssim_multiscale power_factors
+
+struct SsimScaleArgs {
+  const uint8_t* a8;  // scale 0: u8 NHWC (N,H,W,3)
+  const uint8_t* b8;
+  const float* af;    // scales 1..4: planar fp32 (P,H,W)
+  const float* bf;
+  double2* part;      // [P][tiles] (sum ssim, sum cs) per output tile
+  int P, H, W, tiles_x, tiles;
+};
+
+struct SsimCombineArgs {
+  const double2* part;
+  size_t offset[kSsimScales];  // in double2 units
+  int tiles[kSsimScales];
+  int64_t valid[kSsimScales];  // valid filter outputs per plane
+  float* out;                  // (N,)
+  float* per_scale;            // optional (N,3,5,2): mean ssim, mean cs
+};
+
+// Scratch layout of one MS-SSIM evaluation: pooled images of scales 1..4, then the tile sums.
+struct SsimPlan {
+  int h[kSsimScales], w[kSsimScales], tiles_x[kSsimScales], tiles[kSsimScales];
+  int64_t valid[kSsimScales];
+  size_t img_off[kSsimScales];  // bytes
+  size_t part_off[kSsimScales]; // double2 units after img_bytes
+  size_t img_bytes, bytes;
+};
+hipError_t upload_ssim_constants();  // per device, from nic_create
+void ssim_plan(int nimg, int H, int W, SsimPlan* plan);
+hipError_t launch_ms_ssim(const uint8_t* a, const uint8_t* b, int nimg, int H, int W, void* scratch, float* out,
+                          float* per_scale, hipStream_t st);
+hipError_t launch_sq_err(const uint8_t* a, const uint8_t* b, int nimg, int64_t bytes, unsigned long long* sse,
+                         hipStream_t st);
+
 }  // namespace nic

@@ -313,15 +313,14 @@ def _ssim_per_channel(x, y, max_val=1.0, k1=0.01, k2=0.03, kernel=None):
     return (luminance * cs).mean(axis=(1, 2)), cs.mean(axis=(1, 2))
 
 
-def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
-    """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,).
-
-    Like TF, the coarsest of the 5 scales must still hold the 11x11 window: H, W >= 176."""
+def ms_ssim_terms(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
+    """Per-scale terms of ms_ssim: (N,C,5,2) float64 = (mean SSIM, mean cs) per channel and
+    scale, before the relu and the weighted geometric mean."""
     if min(img1.shape[1], img1.shape[2]) < 11 * 2 ** (len(MSSSIM_WEIGHTS) - 1):
         raise ValueError(f"MS-SSIM needs images of at least 176x176, got {img1.shape[1:3]}")
     x = img1.astype(np.float64) * np.float32(1.0 / 255)
     y = img2.astype(np.float64) * np.float32(1.0 / 255)
-    mcs = []
+    terms = []
     for k in range(len(MSSSIM_WEIGHTS)):
         if k > 0:
             h, w = x.shape[1], x.shape[2]
@@ -330,8 +329,15 @@ def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
                 x, y = np.pad(x, pad, mode="symmetric"), np.pad(y, pad, mode="symmetric")
             x = 0.25 * (x[:, 0::2, 0::2] + x[:, 1::2, 0::2] + x[:, 0::2, 1::2] + x[:, 1::2, 1::2])
             y = 0.25 * (y[:, 0::2, 0::2] + y[:, 1::2, 0::2] + y[:, 0::2, 1::2] + y[:, 1::2, 1::2])
-        ssim_c, cs = _ssim_per_channel(x, y)
-        mcs.append(np.maximum(cs, 0))
-    mcs.pop()
-    stack = np.stack(mcs + [np.maximum(ssim_c, 0)], axis=-1)
-    return np.prod(stack ** np.asarray(MSSSIM_WEIGHTS), axis=-1).mean(axis=-1)
+        terms.append(np.stack(_ssim_per_channel(x, y), axis=-1))
+    return np.stack(terms, axis=2)
+
+
+def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
+    """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,).
+
+    Like TF, the coarsest of the 5 scales must still hold the 11x11 window: H, W >= 176."""
+    t = ms_ssim_terms(img1, img2)
+    # cs of scales 0..3 and SSIM of the last scale, each relu'd
+    mcs = np.concatenate([t[:, :, :-1, 1], t[:, :, -1:, 0]], axis=-1)
+    return np.prod(np.maximum(mcs, 0) ** np.asarray(MSSSIM_WEIGHTS), axis=-1).mean(axis=-1)
