@@ -280,12 +280,13 @@ class Encoder(ProClass):
     def _device_call(self, x):
         return self.codec.encode(x)
 
-    def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4) -> None:
-        """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``."""
+    def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
+        """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``.
+        ``workers``: host threads for the PNG writes (0 = inline, as the reference)."""
         from .bitstream import use_model
 
         use_model(self, dataset_path, checkpoint_path, dataset_path + "_compressed", in_cshape=3,
-                  batch_size=batch_size)
+                  batch_size=batch_size, workers=workers)
 
 
 class Decoder(ProClass):
@@ -296,9 +297,9 @@ class Decoder(ProClass):
     def _device_call(self, z):
         return self.codec.decode(z)
 
-    def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4) -> None:
+    def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
         """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``."""
         from .bitstream import use_model
 
         use_model(self, dataset_path, checkpoint_path, dataset_path.replace("compressed", "uncompressed"),
-                  in_cshape=96, batch_size=batch_size)
+                  in_cshape=96, batch_size=batch_size, workers=workers)

@@ -267,6 +267,16 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     dec.uncompress(str(tmp_path / "kodak_compressed"), str(tmp_path / "ckpt" / "decoder"))
     rec = np.array(Image.open(tmp_path / "kodak_uncompressed" / "img1.png"))
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
+    # threaded PNG writes (workers > 0) produce byte-identical files
+    ds2 = tmp_path / "thr"
+    ds2.mkdir()
+    for i in range(3):
+        Image.fromarray(g["x"][i]).save(ds2 / f"img{i}.png")
+    enc.compress(str(ds2), ck, batch_size=2, workers=3)
+    dec.uncompress(str(tmp_path / "thr_compressed"), str(tmp_path / "ckpt" / "decoder"), workers=2)
+    for i in range(3):
+        for a, b in (("kodak_compressed", "thr_compressed"), ("kodak_uncompressed", "thr_uncompressed")):
+            assert (tmp_path / a / f"img{i}.png").read_bytes() == (tmp_path / b / f"img{i}.png").read_bytes()
 
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}],

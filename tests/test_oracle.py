@@ -171,3 +171,14 @@ def test_ms_ssim_properties(golden):
     assert k.shape == (11, 11) and k.sum() == pytest.approx(1.0) and k[5, 5] == k.max()
     with pytest.raises(ValueError):
         O.ms_ssim(x[:, :128, :128], x[:, :128, :128])
+
+
+def test_tile_patches_roundtrip():
+    from neural_network_image_compression_amd.rd import tile_patches, untile_patches
+    x = np.random.default_rng(0).integers(0, 256, (2, 512, 768, 3), dtype=np.uint8)
+    t = tile_patches(x, 256)
+    assert t.shape == (12, 256, 256, 3)
+    np.testing.assert_array_equal(t[4], x[0, 256:512, 256:512])
+    np.testing.assert_array_equal(untile_patches(t, 2, 512, 768), x)
+    with pytest.raises(ValueError):
+        tile_patches(x[:, :300], 256)
