@@ -206,13 +206,39 @@ def save(w: Weights, path_prefix: str, kind: str) -> List[str]:
     return paths
 
 
+def save_tf(w: Weights, path_prefix: str, kind: str) -> List[str]:
+    """The reference's own format: ``Model.save_weights(path_prefix + name)`` for name in
+    Y, CbCr (training.py:167-170), i.e. TF object-based tensor bundles keyed
+    ``<layer>/<kernel|bias>/.ATTRIBUTES/VARIABLE_VALUE`` (see tfckpt.py)."""
+    from . import tfckpt
+
+    paths = []
+    for name, sub in split_models(w, kind).items():
+        m = kind + name + "/"
+        tensors = {k[len(m):] + tfckpt.VARIABLE_SUFFIX: np.asarray(v, np.float32) for k, v in sub.items()}
+        paths += tfckpt.write_bundle(path_prefix + name, tensors)
+    return paths
+
+
 def load(path_prefix: str, kind: str) -> Weights:
-    """Inverse of :func:`save`; mirrors ProClass.load (utils.py:26-28)."""
+    """Inverse of :func:`save`; mirrors ProClass.load (utils.py:26-28).
+
+    ``path_prefix + name`` may also be a TF checkpoint written by the reference's
+    ``save_weights`` (``<prefix><name>.index`` + ``.data-*``), read without TensorFlow."""
     from safetensors.numpy import load_file
+
+    from . import tfckpt
 
     w: Weights = {}
     for name in PLANE_MODELS:
         p = path_prefix + name
+        if not p.endswith(".safetensors") and os.path.exists(p + ".index"):
+            layers = tfckpt.keras_layer_tensors(tfckpt.read_bundle(p))
+            names = {spec.name for spec in (ENCODER_LAYERS if kind == "encoder" else DECODER_LAYERS)}
+            for k, v in layers.items():
+                if k.split("/")[0] in names:
+                    w[kind + name + "/" + k] = np.asarray(v, np.float32)
+            continue
         if not p.endswith(".safetensors"):
             p += ".safetensors"
         sub = load_file(p)

@@ -1,0 +1,78 @@
+"""TF tensor-bundle checkpoints (tfckpt.py): the reference's save_weights / load_weights
+format (training.py:167-170, utils.py:26-28), read and written without TensorFlow.
+
+Parity with checkpoints written by TensorFlow itself is unpinned (none ship with the
+reference and TF is not installable); these tests pin the restated format pieces that
+have published known answers (CRC32C check value, LevelDB masking) and the round trip."""
+import os
+
+import numpy as np
+import pytest
+
+from neural_network_image_compression_amd import tfckpt
+from neural_network_image_compression_amd import weights as W
+
+
+def test_crc32c_known_answers():
+    assert tfckpt.crc32c(b"123456789") == 0xE3069283  # CRC-32C check value
+    assert tfckpt.crc32c(b"\x00" * 32) == 0x8A9136AA  # RFC 3720 B.4 test vector
+    assert tfckpt.crc32c(bytes(range(32))) == 0x46DD794E
+    assert tfckpt.mask_crc(0) == 0xA282EAD8
+
+
+def test_entry_proto_roundtrip():
+    raw = tfckpt.encode_entry(1, (5, 5, 32, 64), 1234, 204800, 0xDEADBEEF)
+    e = tfckpt.parse_entry(raw)
+    assert e["dtype"] == 1 and e["shape"] == [5, 5, 32, 64] and e["offset"] == 1234
+    assert e["size"] == 204800 and e["crc32c"] == 0xDEADBEEF and not e["sliced"]
+
+
+def test_table_many_keys_roundtrip(tmp_path):
+    entries = {f"layer{i:03d}/kernel/.ATTRIBUTES/VARIABLE_VALUE": bytes([i % 256]) * (i % 7) for i in range(100)}
+    entries[""] = b"\x08\x01"
+    p = str(tmp_path / "t.index")
+    tfckpt.write_table(p, entries)
+    assert tfckpt.read_table(p) == entries
+    data = bytearray(open(p, "rb").read())
+    data[10] ^= 1
+    open(p, "wb").write(bytes(data))
+    with pytest.raises(ValueError):
+        tfckpt.read_table(p)
+
+
+def test_bundle_roundtrip_dtypes(tmp_path):
+    rng = np.random.default_rng(0)
+    t = {"a/kernel/.ATTRIBUTES/VARIABLE_VALUE": rng.standard_normal((3, 3, 4, 5)).astype(np.float32),
+         "a/bias/.ATTRIBUTES/VARIABLE_VALUE": rng.standard_normal(5).astype(np.float32),
+         "save_counter/.ATTRIBUTES/VARIABLE_VALUE": np.array(7, np.int64),
+         "b/kernel/.OPTIMIZER_SLOT/optimizer/m/.ATTRIBUTES/VARIABLE_VALUE": np.ones((2,), np.float32)}
+    prefix = str(tmp_path / "ck" / "encoderY")
+    tfckpt.write_bundle(prefix, t)
+    back = tfckpt.read_bundle(prefix)
+    assert set(back) == set(t)
+    for k in t:
+        np.testing.assert_array_equal(back[k], t[k])
+        assert back[k].dtype == t[k].dtype
+    assert set(tfckpt.keras_layer_tensors(back)) == {"a/kernel", "a/bias"}
+    # a flipped data byte fails the per-tensor CRC
+    dp = prefix + ".data-00000-of-00001"
+    raw = bytearray(open(dp, "rb").read())
+    raw[3] ^= 0x40
+    open(dp, "wb").write(bytes(raw))
+    with pytest.raises(ValueError):
+        tfckpt.read_bundle(prefix)
+
+
+def test_codec_weights_via_tf_checkpoint(tmp_path):
+    """ProClass.load(path) reads path+'Y' / path+'CbCr' TF checkpoints like Keras load_weights."""
+    w = W.seeded_weights(3)
+    for kind in ("encoder", "decoder"):
+        prefix = str(tmp_path / "checkpoints" / kind)
+        paths = W.save_tf(w, prefix, kind)
+        assert os.path.exists(prefix + "Y.index") and os.path.exists(prefix + "CbCr.data-00000-of-00001")
+        assert len(paths) == 4
+        back = W.load(prefix, kind)
+        sub = {k: v for k, v in w.items() if k.startswith(kind)}
+        assert set(back) == set(sub)
+        for k in sub:
+            np.testing.assert_array_equal(back[k], sub[k])
