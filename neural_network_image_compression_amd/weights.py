@@ -234,10 +234,15 @@ def load(path_prefix: str, kind: str) -> Weights:
         p = path_prefix + name
         if not p.endswith(".safetensors") and os.path.exists(p + ".index"):
             layers = tfckpt.keras_layer_tensors(tfckpt.read_bundle(p))
-            names = {spec.name for spec in (ENCODER_LAYERS if kind == "encoder" else DECODER_LAYERS)}
+            order = [spec.name for spec in (ENCODER_LAYERS if kind == "encoder" else DECODER_LAYERS)]
             for k, v in layers.items():
-                if k.split("/")[0] in names:
-                    w[kind + name + "/" + k] = np.asarray(v, np.float32)
+                lname, var = k.split("/")
+                # subclassed models key by attribute (conv1/...); functional / Sequential
+                # saves key by position (layer_with_weights-0/...)
+                if lname.startswith("layer_with_weights-") and lname[19:].isdigit() and int(lname[19:]) < len(order):
+                    lname = order[int(lname[19:])]
+                if lname in order:
+                    w[kind + name + "/" + lname + "/" + var] = np.asarray(v, np.float32)
             continue
         if not p.endswith(".safetensors"):
             p += ".safetensors"

@@ -76,3 +76,16 @@ def test_codec_weights_via_tf_checkpoint(tmp_path):
         assert set(back) == set(sub)
         for k in sub:
             np.testing.assert_array_equal(back[k], sub[k])
+
+
+def test_positional_layer_keys(tmp_path):
+    """Functional / Sequential saves key layers as layer_with_weights-N (encoder.py:10-17 order)."""
+    w = W.seeded_weights(4)
+    order = ["conv1", "conv2", "conv3", "conv4", "conv8"]
+    for name in W.PLANE_MODELS:
+        t = {f"layer_with_weights-{i}/{var}" + tfckpt.VARIABLE_SUFFIX: w[f"encoder{name}/{l}/{var}"]
+             for i, l in enumerate(order) for var in ("kernel", "bias")}
+        tfckpt.write_bundle(str(tmp_path / ("enc" + name)), t)
+    back = W.load(str(tmp_path / "enc"), "encoder")
+    for k, v in back.items():
+        np.testing.assert_array_equal(v, w[k])
