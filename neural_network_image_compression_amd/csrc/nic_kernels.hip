@@ -2471,12 +2471,13 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
   const int bin = threadIdx.x & 255, g = threadIdx.x >> 8;
   const uint32_t* src = part + (size_t)p * chunks * 256 + bin;
   uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int k = g;
-  for (; k + 28 < chunks; k += 32) {
+  for (int k0 = g; k0 < chunks; k0 += 64) {  // 16 predicated loads in flight per round
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += src[(size_t)(k + 4 * u) * 256];
+    for (int u = 0; u < 16; ++u) {
+      const int k = k0 + 4 * u;
+      acc[u & 7] += k < chunks ? src[(size_t)k * 256] : 0u;
+    }
   }
-  for (; k < chunks; k += 4) acc[0] += src[(size_t)k * 256];
   uint32_t c = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (g) grp[g - 1][bin] = c;
   __syncthreads();
@@ -2606,6 +2607,17 @@ static int device_cus() {
   return cache[d];
 }
 
+// Resident blocks per CU of the stride-1 weight-stationary launches (51 KB LDS, <= 128
+// VGPRs: up to 3 fit); NIC_WS_BPC overrides for A/B runs.
+static int ws_k3_blocks_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("NIC_WS_BPC");
+    const int n = e ? atoi(e) : 2;
+    return n >= 1 && n <= 3 ? n : 2;
+  }();
+  return v;
+}
+
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
 // in proportion to each group's MFMA work (planes x taps).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
@@ -2627,7 +2639,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
     work[gi] = planes * per_plane * (2 * taps[gi >> 1] + (PROJ ? 1 : 0));  // + projection: 12 of 24/tap MFMAs
     total += work[gi];
   }
-  const int target = 2 * device_cus();
+  const int target = (TRP ? 2 : ws_k3_blocks_per_cu()) * device_cus();
   a.ws_blk[0] = 0;
   for (int gi = 0; gi < a.ws_ngrp; ++gi) {
     const long long tiles = ((gi & 1) ? a.P - a.nimg : a.nimg) * per_plane;
@@ -2785,7 +2797,9 @@ hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part,
   int chunk_vec;
   const int chunks = hist_chunks(nimg, plane_px, &chunk_vec);
   const char* hv = getenv("NIC_HIST");
-  const char m = hv ? hv[0] : '8';  // A/B switch (tools/hist_ab.py); 8 replicas measured best
+  // A/B switch (tools/hist_ab.py): 8 replicas measured best (a packed-u16 32-replica
+  // layout, conflict-free by construction, was 15 % slower)
+  const char m = hv ? hv[0] : '8';
   const bool zb = hv && hv[1] == 'z';
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(256), 0, st, z, nimg, plane_px, part, chunk_vec);

@@ -173,6 +173,21 @@ def test_entropy_large_and_edge_planes(codecs):
     assert bits[1].item() == 0.0
 
 
+def test_entropy_counter_capacity(codecs):
+    """16 constant 4K latents: the largest latent chunk per histogram block (16,384
+    16-B vectors), every code of a plane in one bin -- the worst case for LDS atomic
+    collisions and for the per-block partial counts."""
+    z = torch.full((16, 270, 480, 96), 200, dtype=torch.uint8, device="cuda")
+    z[..., 32:64] = 201
+    bits, cnt = codecs["spread"].entropy(z, counts=True)
+    cnt = cnt.cpu().numpy()
+    expect = np.zeros((48, 256), np.int64)
+    expect[:16, 200] = expect[32:, 200] = expect[16:32, 201] = 270 * 480 * 32
+    np.testing.assert_array_equal(cnt, expect)
+    assert float(bits.abs().max()) == 0.0
+    del z
+
+
 def test_pack_unpack_bit_exact(codecs):
     rng = np.random.default_rng(9)
     z = rng.integers(0, 256, (3, 7, 5, 96), dtype=np.uint8)
