@@ -156,37 +156,30 @@ __global__ __launch_bounds__(256) void ssim_pool_kernel(SsimScaleArgs a, float* 
   }
 }
 
-// One block per image: tile sums -> per-(channel, scale) means -> weighted geometric mean.
-__global__ __launch_bounds__(256) void msssim_combine_kernel(SsimCombineArgs a) {
-  __shared__ double red[2][4];
+// One block per image, one wave per (channel, scale): tile sums -> means (all 15 waves
+// load at once), then thread 0 forms the weighted geometric mean.
+constexpr int kCombineWaves = 3 * kSsimScales;
+__global__ __launch_bounds__(64 * kCombineWaves) void msssim_combine_kernel(SsimCombineArgs a) {
   __shared__ double mean[3][kSsimScales][2];
-  const int img = blockIdx.x, tid = threadIdx.x;
-  for (int ch = 0; ch < 3; ++ch) {
-    const int p = img * 3 + ch;
-    for (int k = 0; k < kSsimScales; ++k) {
-      const double2* part = a.part + a.offset[k] + (size_t)p * a.tiles[k];
-      double s = 0.0, c = 0.0;
-      for (int t = tid; t < a.tiles[k]; t += 256) {
-        s += part[t].x;
-        c += part[t].y;
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        s += __shfl_xor(s, o, 64);
-        c += __shfl_xor(c, o, 64);
-      }
-      if ((tid & 63) == 0) {
-        red[0][tid >> 6] = s;
-        red[1][tid >> 6] = c;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        const double cnt = (double)a.valid[k];
-        mean[ch][k][0] = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / cnt;
-        mean[ch][k][1] = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / cnt;
-      }
-      __syncthreads();
+  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  {
+    const int ch = w / kSsimScales, k = w % kSsimScales;
+    const double2* part = a.part + a.offset[k] + (size_t)(img * 3 + ch) * a.tiles[k];
+    double s = 0.0, c = 0.0;
+    for (int t = lane; t < a.tiles[k]; t += 64) {
+      s += part[t].x;
+      c += part[t].y;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      c += __shfl_xor(c, o, 64);
+    }
+    if (lane == 0) {
+      mean[ch][k][0] = s / (double)a.valid[k];
+      mean[ch][k][1] = c / (double)a.valid[k];
     }
   }
+  __syncthreads();
   if (tid == 0) {
     double acc = 0.0;
     for (int ch = 0; ch < 3; ++ch) {
@@ -333,7 +326,7 @@ hipError_t launch_ms_ssim(const uint8_t* a, const uint8_t* b, int nimg, int H, i
   }
   c.out = out;
   c.per_scale = per_scale;
-  hipLaunchKernelGGL(msssim_combine_kernel, dim3(nimg), dim3(256), 0, st, c);
+  hipLaunchKernelGGL(msssim_combine_kernel, dim3(nimg), dim3(64 * kCombineWaves), 0, st, c);
   return hipGetLastError();
 }
 
