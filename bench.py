@@ -110,7 +110,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first: kernel durations settle over the first ~15 steps (clocks)")
     ap.add_argument("--batch", type=int, default=None, help="images (frames) per GPU per step")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--workload", default="config2", choices=["config2", "kodak", "4k"],

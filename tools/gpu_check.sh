@@ -25,7 +25,7 @@ if [[ "$STEPS" == all || "$STEPS" == *smoke* ]]; then
   rc=$?; tail -5 "$OUT/${TAG}_smoke.log"; stop_on $rc smoke
 fi
 if [[ "$STEPS" == all || "$STEPS" == *bench* ]]; then
-  timeout -k 10 300 python bench.py --steps 20 --warmup 3 > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
+  timeout -k 10 300 python bench.py --steps 20 --warmup 10 > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
   rc=$?; cat "$OUT/${TAG}_bench.json"; tail -5 "$OUT/${TAG}_bench.err"; stop_on $rc bench
 fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
