@@ -231,6 +231,23 @@ def main():
                    "ms_ssim_gbps_scale0": round(nbytes / (q_ms * 1e-3) / 1e9, 1),
                    "kernels": "ssim_tile_kernel x5 scales + ssim_pool_kernel x4 + msssim_combine_kernel"}
 
+    coll = None
+    if world > 1:
+        # config 3's exchange, outside the timed steps: the shards' u8 latents
+        # (and recons) gathered to rank 0 over RCCL in global order (parallel.gather_rows)
+        from neural_network_image_compression_amd.parallel import gather_rows
+        outs = [z] if args.workload == "4k" else [z, r]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in outs:
+            gather_rows(t, world * B, dist, dst=0)
+        torch.cuda.synchronize()
+        barrier()
+        coll = {"gather_ms": round((time.perf_counter() - t0) * 1e3, 3),
+                "gathered_bytes": int(world * B * sum(t[0].numel() for t in outs)),
+                "op": "all_gather of padded shards (RCCL) of the u8 latents" +
+                      ("" if args.workload == "4k" else " and recons") + ", once after the timed steps"}
     if rank != 0:
         barrier()
         if world > 1:
@@ -312,6 +329,8 @@ def main():
     }
     if quality is not None:
         out["quality"] = quality
+    if coll is not None:
+        out["collectives"] = coll
     if args.workload == "4k":
         out["metric"] = "Megapixels/sec encode + entropy (4K frames)"
         out["frames_per_s"] = round(world * B * args.steps / el, 2)

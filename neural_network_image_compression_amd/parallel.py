@@ -88,3 +88,21 @@ def gather_rows(local, n_total: int, dist, dst: Optional[int] = 0):
         a, b = shard_range(n_total, world, r)
         parts.append(blocks[r][: b - a])
     return torch.cat(parts, dim=0)
+
+
+def run_sharded(codec, x_local, n_total: int, dist, dst: Optional[int] = 0, entropy: bool = True):
+    """BASELINE config 3 on one rank: encode -> decode (and histogram entropy) of this
+    rank's shard on its own GPU, then the shards' u8 latents (N,h,w,96), u8 recons
+    (N,8h,8w,3) and per-image entropy rows (N,3) gathered to ``dst`` in global order.
+
+    ``codec`` is a :class:`codec.Codec` on this rank's device (or any object with the same
+    encode / decode / entropy methods).  Returns (latents, recons, bits) on ``dst`` (bits is
+    None without ``entropy``), (None, None, None) elsewhere."""
+    z = codec.encode(x_local)
+    r = codec.decode(z)
+    n = x_local.shape[0]
+    bits = codec.entropy(z).view(3, n).t().contiguous() if entropy else None  # plane-major -> (n, 3)
+    zg = gather_rows(z, n_total, dist, dst)
+    rg = gather_rows(r, n_total, dist, dst)
+    bg = gather_rows(bits, n_total, dist, dst) if entropy else None
+    return zg, rg, bg
