@@ -20,6 +20,8 @@ namespace nic {
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 constexpr int kSsimTile = 32;                    // output tile edge
 constexpr int kSsimTaps = 11;                    // Gaussian window (TF filter_size)
 constexpr int kSsimIn = kSsimTile + kSsimTaps - 1;  // 42: input window edge
@@ -46,65 +48,109 @@ __global__ __launch_bounds__(256) void ssim_tile_kernel(SsimScaleArgs a) {
   const int y0 = ty * kSsimTile, x0 = tx * kSsimTile;
   const int OH = a.H - kSsimTaps + 1, OW = a.W - kSsimTaps + 1;
 
-  for (int i = tid; i < kSsimIn * kSsimIn; i += 256) {
+  // window load: every element's global load issued before any is used (one latency
+  // round per block instead of one per 256 elements)
+  constexpr int kLoads = (kSsimIn * kSsimIn + 255) / 256;
+  float lx[kLoads], ly[kLoads];
+#pragma unroll
+  for (int k = 0; k < kLoads; ++k) {
+    const int i = tid + 256 * k;
     const int r = i / kSsimIn, c = i % kSsimIn;
     const int y = y0 + r, x = x0 + c;
-    float vx = 0.f, vy = 0.f;
-    if (y < a.H && x < a.W) {
+    lx[k] = 0.f;
+    ly[k] = 0.f;
+    if (i < kSsimIn * kSsimIn && y < a.H && x < a.W) {
       if constexpr (U8) {
         const int img = p / 3, ch = p % 3;
         const size_t o = ((size_t)(img * a.H + y) * a.W + x) * 3 + ch;
-        // convert_image_dtype: u8 * (1/255) in fp32
-        vx = (float)a.a8[o] * (1.0f / 255.0f) - 0.5f;
-        vy = (float)a.b8[o] * (1.0f / 255.0f) - 0.5f;
+        lx[k] = (float)a.a8[o];
+        ly[k] = (float)a.b8[o];
       } else {
         const size_t o = ((size_t)p * a.H + y) * a.W + x;
-        vx = a.af[o] - 0.5f;
-        vy = a.bf[o] - 0.5f;
+        lx[k] = a.af[o];
+        ly[k] = a.bf[o];
       }
     }
-    sx[r][c] = vx;
-    sy[r][c] = vy;
   }
-  __syncthreads();
-
-  for (int i = tid; i < kSsimIn * kSsimTile; i += 256) {
-    const int r = i / kSsimTile, c = i % kSsimTile;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-    for (int j = 0; j < kSsimTaps; ++j) {
-      const float g = c_gauss[j], vx = sx[r][c + j], vy = sy[r][c + j];
-      s0 = fmaf(g, vx, s0);
-      s1 = fmaf(g, vy, s1);
-      s2 = fmaf(g, fmaf(vx, vx, vy * vy), s2);
-      s3 = fmaf(g, vx * vy, s3);
+  for (int k = 0; k < kLoads; ++k) {
+    const int i = tid + 256 * k;
+    if (i < kSsimIn * kSsimIn) {
+      const int r = i / kSsimIn, c = i % kSsimIn;
+      const bool in = y0 + r < a.H && x0 + c < a.W;
+      // convert_image_dtype: u8 * (1/255) in fp32; shifted by -0.5 (0 outside the image)
+      sx[r][c] = in ? (U8 ? lx[k] * (1.0f / 255.0f) : lx[k]) - 0.5f : 0.f;
+      sy[r][c] = in ? (U8 ? ly[k] * (1.0f / 255.0f) : ly[k]) - 0.5f : 0.f;
     }
-    hm[0][r][c] = s0;
-    hm[1][r][c] = s1;
-    hm[2][r][c] = s2;
-    hm[3][r][c] = s3;
   }
   __syncthreads();
 
+  // horizontal pass: an item is 4 consecutive outputs of one row (register window of 14
+  // inputs, the products x^2 + y^2 and xy formed once per input)
+  constexpr int kSeg = 4, kSegs = kSsimTile / kSeg;
+  for (int i = tid; i < kSsimIn * kSegs; i += 256) {
+    const int r = i / kSegs, c0 = (i % kSegs) * kSeg;
+    constexpr int kWin = kSeg + kSsimTaps - 1;
+    // (x, y) and (x^2 + y^2, xy) pairs: the four sums run as two packed fp32 FMA streams
+    f32x2 wxy[kWin], wqp[kWin];
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) {
+      const float vx = sx[r][c0 + j], vy = sy[r][c0 + j];
+      wxy[j] = (f32x2){vx, vy};
+      wqp[j] = (f32x2){fmaf(vx, vx, vy * vy), vx * vy};
+    }
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      f32x2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < kSsimTaps; ++j) {
+        const f32x2 g = {c_gauss[j], c_gauss[j]};
+        s01 = __builtin_elementwise_fma(g, wxy[o + j], s01);
+        s23 = __builtin_elementwise_fma(g, wqp[o + j], s23);
+      }
+      hm[0][r][c0 + o] = s01[0];
+      hm[1][r][c0 + o] = s01[1];
+      hm[2][r][c0 + o] = s23[0];
+      hm[3][r][c0 + o] = s23[1];
+    }
+  }
+  __syncthreads();
+
+  // vertical pass: an item is 4 consecutive rows of one column (window of 14 rows)
   const float c1 = 0.01f * 0.01f, c2 = 0.03f * 0.03f;  // (k1 * max_val)^2, (k2 * max_val)^2, max_val = 1
   float ssum = 0.f, csum = 0.f;
-  for (int i = tid; i < kSsimTile * kSsimTile; i += 256) {
-    const int r = i / kSsimTile, c = i % kSsimTile;
-    if (y0 + r >= OH || x0 + c >= OW) continue;
-    float m0 = 0.f, m1 = 0.f, e2 = 0.f, e3 = 0.f;
+  for (int i = tid; i < kSsimTile * kSegs; i += 256) {
+    const int c = i % kSsimTile, r0 = (i / kSsimTile) * kSeg;
+    f32x2 a01[kSeg], a23[kSeg];
 #pragma unroll
-    for (int j = 0; j < kSsimTaps; ++j) {
-      const float g = c_gauss[j];
-      m0 = fmaf(g, hm[0][r + j][c], m0);
-      m1 = fmaf(g, hm[1][r + j][c], m1);
-      e2 = fmaf(g, hm[2][r + j][c], e2);
-      e3 = fmaf(g, hm[3][r + j][c], e3);
+    for (int o = 0; o < kSeg; ++o) {
+      a01[o] = (f32x2){0.f, 0.f};
+      a23[o] = (f32x2){0.f, 0.f};
     }
-    const float mx = m0 + 0.5f, my = m1 + 0.5f;
-    const float lum = (2.f * mx * my + c1) / (mx * mx + my * my + c1);
-    const float cs = (2.f * (e3 - m0 * m1) + c2) / (e2 - (m0 * m0 + m1 * m1) + c2);
-    ssum += lum * cs;
-    csum += cs;
+#pragma unroll
+    for (int j = 0; j < kSeg + kSsimTaps - 1; ++j) {
+      const f32x2 v01 = {hm[0][r0 + j][c], hm[1][r0 + j][c]}, v23 = {hm[2][r0 + j][c], hm[3][r0 + j][c]};
+#pragma unroll
+      for (int o = 0; o < kSeg; ++o) {
+        const int t = j - o;  // tap of input row r0 + j for output row r0 + o
+        if (t >= 0 && t < kSsimTaps) {
+          const f32x2 g = {c_gauss[t], c_gauss[t]};
+          a01[o] = __builtin_elementwise_fma(g, v01, a01[o]);
+          a23[o] = __builtin_elementwise_fma(g, v23, a23[o]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      if (y0 + r0 + o >= OH || x0 + c >= OW) continue;
+      const float m0 = a01[o][0], m1 = a01[o][1], e2 = a23[o][0], e3 = a23[o][1];
+      const float mx = m0 + 0.5f, my = m1 + 0.5f;
+      // v_rcp_f32 (1 ulp) instead of the IEEE division sequence
+      const float lum = (2.f * mx * my + c1) * __builtin_amdgcn_rcpf(mx * mx + my * my + c1);
+      const float cs = (2.f * (e3 - m0 * m1) + c2) * __builtin_amdgcn_rcpf(e2 - (m0 * m0 + m1 * m1) + c2);
+      ssum += lum * cs;
+      csum += cs;
+    }
   }
   ssum = wave_sum(ssum);
   csum = wave_sum(csum);
