@@ -62,6 +62,10 @@ def test_null_arguments_are_rejected_without_crashing():
     assert L.nic_pack_latent(None, 1, 0, 1, None, None) == _lib.NIC_ESHAPE
     assert L.nic_pack_latent(None, 0, 1, 1, None, None) == _lib.NIC_OK  # empty batch
     assert L.nic_set_timing(None, 1) == _lib.NIC_EINVAL
+    assert L.nic_ms_ssim(None, None, None, 1, 256, 256, None, None, None) == _lib.NIC_EINVAL
+    assert L.nic_sq_err(None, None, -1, 10, None, None) == _lib.NIC_ESHAPE
+    assert L.nic_sq_err(None, None, 2, 10, None, None) == _lib.NIC_EINVAL
+    assert L.nic_sq_err(None, None, 0, 10, None, None) == _lib.NIC_OK  # empty batch
     assert L.nic_destroy(None) == _lib.NIC_OK
 
 
