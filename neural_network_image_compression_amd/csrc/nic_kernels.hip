@@ -1967,11 +1967,16 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 // projection planes.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
-  const int n = blockIdx.y;
-  const int tyi = blockIdx.x / a.tiles_x;
+  // XCD-aware order: blocks are dealt round-robin to the 8 XCDs, so block L runs on XCD
+  // L % 8; give each XCD a contiguous raster range of (image, tile) instead, so neighbouring
+  // tiles -- which read each other's edge projections -- share that XCD's L2
+  const int gx = gridDim.x, total = gx * gridDim.y, L = blockIdx.y * gx + blockIdx.x;
+  const int T = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+  const int n = T / gx, tb = T - n * gx;
+  const int tyi = tb / a.tiles_x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int my = tyi * 16 + 2 * (lane >> 3) + (wave >> 1);
-  const int mx = (blockIdx.x - tyi * a.tiles_x) * 16 + 2 * (lane & 7) + (wave & 1);
+  const int mx = (tb - tyi * a.tiles_x) * 16 + 2 * (lane & 7) + (wave & 1);
   if (my >= a.H || mx >= a.W) return;
   constexpr int TB[4] = {0, 4, 10, 16};  // phase-major tap bases (for_each_phase_tap)
   float outv[3][4];
