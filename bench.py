@@ -14,8 +14,9 @@ Rank 0 prints ONE JSON line with the driver's keys plus:
   roofline     -- dominant kernel: algorithmic FLOP per launch / its mean launch time,
                   measured with hipEvents on the launch stream over a timed pass;
   layers       -- the same per layer;
-  cpu_baseline -- the NumPy oracle (fp32 BLAS, the CPU restatement of tf2_0; TF itself
-                  is not installable) on a bounded sample, rank 0 at N=1 only;
+  cpu_baseline -- the PyTorch-CPU (oneDNN) restatement of tf2_0 on this process's host
+                  cores (TF itself is not installable), bounded sample, rank 0 at N=1 only;
+                  the NumPy oracle's rate beside it as `numpy_oracle`;
   parity       -- PSNR of one benchmarked image's reconstruction vs the oracle.
 """
 from __future__ import annotations
@@ -61,7 +62,30 @@ def layer_geometry(h: int, w: int):
     return g
 
 
-def cpu_baseline(weights, size: int, seconds: float):
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def _host_threads() -> int:
+    """Host cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box; os.cpu_count() there reports the whole machine)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:  # pragma: no cover
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_baseline_numpy(weights, size: int, seconds: float):
     """NumPy oracle (fp32 BLAS accumulation) on synthetic images of the same workload until
     `seconds` of CPU work have run (at least one image)."""
     from oracle import nic_oracle as O
@@ -80,9 +104,59 @@ def cpu_baseline(weights, size: int, seconds: float):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": n * size * size / 1e6 / el, "unit": "MP/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} synthetic {size}x{size}x3 images, encode+decode, oracle/nic_oracle.py fp32 "
-                      f"(CPU restatement of tf2_0; TF not installable), {el:.1f} s"}
+    return {"value": round(n * size * size / 1e6 / el, 4), "unit": "MP/s", "cores": int(cores),
+            "sample": f"{n} synthetic {size}x{size}x3 images, oracle/nic_oracle.py fp32 BLAS, {el:.1f} s"}
+
+
+def cpu_baseline(weights, size: int, seconds: float, batch: int = 4):
+    """SURVEY §8d's CPU baseline: the PyTorch-CPU (oneDNN) restatement of tf2_0's
+    Encoder()(x) -> Decoder()(z) (training.base_encoder / base_decoder with TF-SAME padding,
+    fp32) on all host cores of this process, batches of 4 images (the reference's directory
+    batch, utils.py:53-62), for `seconds` of CPU work.  Not TF2 itself (not installable)."""
+    import torch
+
+    from neural_network_image_compression_amd import training as T
+    from neural_network_image_compression_amd import weights as Wm
+
+    threads = _host_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    params = {m: {k.split("/", 1)[1]: torch.from_numpy(np.ascontiguousarray(v)) for k, v in weights.items()
+                  if k.startswith(m + "/")} for m in Wm.MODEL_ID}
+    inv = torch.from_numpy(np.linalg.inv(np.array(T.YCBCR, np.float64)).astype(np.float32))
+    off = torch.tensor(T.YCBCR_OFF, dtype=torch.float32)
+    rng = np.random.default_rng(1)
+
+    def one_batch():
+        x = torch.from_numpy(rng.integers(0, 256, (batch, size, size, 3), dtype=np.uint8))
+        y, cb, cr = T.colour_planes(x.float() / 255.0)  # encoder.py:39-41
+        zy = T.base_encoder(params["encoderY"], y)
+        zc = T.base_encoder(params["encoderCbCr"], torch.cat([cb, cr]))
+        z = torch.round(torch.cat([zy, zc[:batch], zc[batch:]], 1) * 255).to(torch.uint8)  # encoder.py:45-47
+        zn = z.float() / 255.0  # decoder.py:40-41
+        dy = T.base_decoder(params["decoderY"], zn[:, :32])
+        dc = T.base_decoder(params["decoderCbCr"], torch.cat([zn[:, 32:64], zn[:, 64:]]))
+        planes = torch.cat([dy, dc[:batch], dc[batch:]], 1).permute(0, 2, 3, 1) - off  # decoder.py:45-46
+        rgb = (planes @ inv.t()).clamp(0, 1)
+        return torch.round(rgb * 255).to(torch.uint8)
+
+    try:
+        with torch.inference_mode():
+            one_batch()  # oneDNN primitive creation outside the timed sample
+            n, t0 = 0, time.perf_counter()
+            while True:
+                one_batch()
+                n += batch
+                el = time.perf_counter() - t0
+                if el >= seconds:
+                    break
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(n * size * size / 1e6 / el, 4), "unit": "MP/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"{n} synthetic {size}x{size}x3 images in batches of {batch}, encode+decode, PyTorch-CPU "
+                      f"(oneDNN) restatement of tf2_0 (training.base_encoder/base_decoder, TF-SAME, fp32): "
+                      f"CPU restatement of tf2_0, not TF2 (not installable), {el:.1f} s"}
 
 
 def parity_sample(codec, x0, weights):
@@ -98,7 +172,7 @@ def parity_sample(codec, x0, weights):
     r_ref = O.decode(weights, O.encode(weights, xh))
     out = {"psnr_gpu_vs_oracle_db": round(O.psnr(r, r_ref), 2),
            "psnr_x_gpu_db": round(O.psnr(xh, r), 4), "psnr_x_oracle_db": round(O.psnr(xh, r_ref), 4)}
-    if min(xh.shape[1:3]) >= 176:
+    if min(xh.shape[1:3]) >= 161:
         # MS-SSIM (calc_ssim.py:13) of the GPU reconstruction by the GPU metric, and of the
         # oracle's reconstruction by the oracle's metric
         out["msssim_x_gpu"] = round(float(codec.ms_ssim(x0, torch.from_numpy(r).to(x0.device)).item()), 6)
@@ -228,7 +302,7 @@ def main():
         host_path = {"mp_per_s": round(B * H * W / 1e6 / hp, 1), "ms_per_batch": round(hp * 1e3, 3),
                      "path": "Encoder()(numpy) -> Decoder()(numpy): pageable host arrays, PCIe both ways"}
     quality = None
-    if args.workload in ("config2", "kodak") and min(H, W) >= 176:
+    if args.workload in ("config2", "kodak") and min(H, W) >= 161:
         # device MS-SSIM (nic_ms_ssim) and PSNR (nic_sq_err) of the batch's reconstruction;
         # outside the encode+decode metric, timed with torch events on the current stream
         rec = codec.decode(codec.encode(x))
@@ -262,7 +336,7 @@ def main():
         barrier()
         coll = {"gather_ms": round((time.perf_counter() - t0) * 1e3, 3),
                 "gathered_bytes": int(world * B * sum(t[0].numel() for t in outs)),
-                "op": "all_gather of padded shards (RCCL) of the u8 latents" +
+                "op": "gather to rank 0 of padded shards (RCCL) of the u8 latents" +
                       ("" if args.workload == "4k" else " and recons") + ", once after the timed steps"}
     if rank != 0:
         barrier()
@@ -354,6 +428,7 @@ def main():
         out["frames_per_s"] = round(world * B * args.steps / el, 2)
     if world == 1 and not args.no_cpu_baseline and args.workload == "config2":
         out["cpu_baseline"] = cpu_baseline(weights, S, args.cpu_seconds)
+        out["cpu_baseline"]["numpy_oracle"] = cpu_baseline_numpy(weights, S, args.cpu_seconds / 2)
     if not args.no_parity and args.workload == "config2":
         out["parity"] = parity_sample(codec, x[:1], weights)
     print(json.dumps(out), flush=True)

@@ -49,7 +49,8 @@ enum {
   NIC_ESHAPE = -2,      /* tensor shape does not match the architecture    */
   NIC_ENOWEIGHTS = -3,  /* encode/decode before every tensor was set       */
   NIC_EHIP = -4,        /* HIP runtime error                               */
-  NIC_ENOMEM = -5       /* device allocation failed                        */
+  NIC_ENOMEM = -5,      /* device allocation failed                        */
+  NIC_ERANGE = -6       /* NIC_RANGE_ERROR: a split-f16 activation left the f16 range */
 };
 
 /* model_id values for nic_set_weights (checkpoint names encoder{Y,CbCr}, decoder{Y,CbCr},
@@ -69,9 +70,24 @@ enum {
  *     f16 and weights pre-scaled by 2^k; a*w ~ a_hi*w_hi + a_hi*w_lo + a_lo*w_hi on
  *     v_mfma_f32_16x16x32_f16 / v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Error
  *     ~2^-22 relative per product, i.e. at the level of fp32 accumulation-order
- *     differences.  Requires |activations| < 65504 (f16 range).
+ *     differences.  The split format holds |x| < 65504 (the f16 range): see the range guard.
  * Bias, activations, residuals, colour transforms and quantisers are fp32 in both modes. */
 enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
+
+/* f16 range guard of NIC_PRECISION_F16X3 (the reference, encoder.py:19-32 / decoder.py:19-32,
+ * has no activation bound; trained weights may drive an activation past the f16 range).
+ * Every kernel that stores a split activation tracks max |x| and, at |x| >= 65504 or a
+ * non-finite x, marks the ctx's range word with the pass's epoch.  Then:
+ *   NIC_RANGE_FALLBACK (default) -- every split-f16 encode/decode pass is followed on the
+ *     same stream by the exact-fp32 pass (NIC_PRECISION_FP32 kernels) gated on that mark:
+ *     its kernels exit at once unless the split pass tripped, in which case they recompute
+ *     and overwrite every output.  No host synchronisation; results always fp32-class.
+ *   NIC_RANGE_ERROR -- the call synchronises its stream after the split pass and returns
+ *     NIC_ERANGE if it tripped (outputs undefined).
+ * nic_range_trips (synchronising) counts the passes that tripped since nic_create. */
+enum { NIC_RANGE_FALLBACK = 0, NIC_RANGE_ERROR = 1 };
+int nic_set_range_policy(nic_ctx* ctx, int policy);
+int nic_range_trips(nic_ctx* ctx, int64_t* passes);
 
 /* ABI version: major * 10000 + minor * 100 + patch */
 int nic_version(void);
@@ -129,7 +145,7 @@ int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8,
 /* MS-SSIM of tf.image.ssim_multiscale(a, b, max_val=255) (tf2_0/tests/calc_ssim.py:13)
  * per image: a, b u8 (n,h,w,3) -> ms_ssim (n,) fp32.  TF defaults: 11-tap Gaussian
  * (sigma 1.5), k1 0.01, k2 0.03, power factors (0.0448, 0.2856, 0.3001, 0.2363, 0.1333),
- * SYMMETRIC-padded 2x2 average pooling between scales; h, w >= 176.
+ * SYMMETRIC-padded 2x2 average pooling between scales; every scale >= 11 px: h, w >= 161.
  * per_scale (nullable): (n,3,5,2) fp32 mean SSIM and mean cs per channel and scale.
  * fp32 filtering, fp64 reductions.  Needs a ctx only for its scratch. */
 int nic_ms_ssim(nic_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int h, int w, float* ms_ssim,

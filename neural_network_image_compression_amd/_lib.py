@@ -30,6 +30,9 @@ NIC_ESHAPE = -2
 NIC_ENOWEIGHTS = -3
 NIC_EHIP = -4
 NIC_ENOMEM = -5
+NIC_ERANGE = -6
+
+RANGE_POLICIES = {"fallback": 0, "error": 1}  # nic.h NIC_RANGE_FALLBACK / NIC_RANGE_ERROR
 
 _lib: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()
@@ -55,6 +58,8 @@ _SIGNATURES = {
     "nic_entropy_hist": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_get_precision": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),
+    "nic_set_range_policy": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "nic_range_trips": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int64)]),
     "nic_set_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_layer_times": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "nic_ms_ssim": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),

@@ -107,6 +107,20 @@ class Codec:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, got {mode!r}")
         _lib.check(self._L.nic_set_precision(self._h, _lib.PRECISIONS[mode]), "nic_set_precision")
 
+    def set_range_policy(self, policy: str) -> None:
+        """f16 range guard of the split-f16 mode (include/nic.h NIC_RANGE_*): 'fallback'
+        (default; a tripped pass is recomputed by the exact-fp32 kernels on the device) or
+        'error' (the call synchronises and raises NicError(NIC_ERANGE))."""
+        if policy not in _lib.RANGE_POLICIES:
+            raise ValueError(f"range policy must be one of {sorted(_lib.RANGE_POLICIES)}, got {policy!r}")
+        _lib.check(self._L.nic_set_range_policy(self._h, _lib.RANGE_POLICIES[policy]), "nic_set_range_policy")
+
+    def range_trips(self) -> int:
+        """Encode/decode passes whose split-f16 activations left the f16 range (synchronises)."""
+        n = ctypes.c_int64()
+        _lib.check(self._L.nic_range_trips(self._h, ctypes.byref(n)), "nic_range_trips")
+        return int(n.value)
+
     def set_timing(self, enable: bool) -> None:
         """Bracket every layer launch with hipEvents on the launch stream (resets the sums)."""
         _lib.check(self._L.nic_set_timing(self._h, int(bool(enable))), "nic_set_timing")
@@ -191,6 +205,8 @@ class Codec:
         for t in (a, b):
             if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or t.device.type != "cuda":
                 raise TypeError("sq_err: expected cuda torch.uint8 tensors")
+            if t.device.index != self.device:  # nic_sq_err launches on this codec's stream
+                raise ValueError(f"sq_err: tensor on cuda:{t.device.index}, codec on cuda:{self.device}")
         if a.shape != b.shape or a.ndim < 1:
             raise ValueError(f"sq_err: shapes differ {tuple(a.shape)} vs {tuple(b.shape)}")
         a, b = a.contiguous(), b.contiguous()

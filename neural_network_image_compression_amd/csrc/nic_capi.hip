@@ -261,6 +261,13 @@ struct nic_ctx {
   // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
   uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
+  // f16 range guard (nic.h NIC_RANGE_*): device words [flag, re-run count], the epoch of the
+  // latest split-f16 pass, the policy, a pinned host word for the ERROR policy's check
+  int* range = nullptr;
+  int* range_host = nullptr;
+  int epoch = 0;
+  int range_policy = NIC_RANGE_FALLBACK;
+  long long error_trips = 0;
   char* zero16 = nullptr;  // 256 zero bytes: DMA source for halo padding
   bool have_k[4][5] = {};
   bool have_b[4][5] = {};
@@ -407,10 +414,6 @@ struct LayerTimer {
     if (_rc) return _rc;                           \
   } while (0)
 
-hipError_t run_layer(const nic_ctx* c, LayerId id, const ConvArgs& a, hipStream_t st) {
-  return c->precision == NIC_PRECISION_F16X3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st);
-}
-
 bool models_ready(const nic_ctx* c, int m0) {
   for (int m = m0; m < m0 + 2; ++m)
     for (int i = 0; i < 5; ++i)
@@ -479,6 +482,11 @@ int nic_create(int device, nic_ctx** out) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
   }
+  if (hipMalloc(&c->range, 2 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 2 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    nic_destroy(c);
+    return fail(NIC_ENOMEM, "nic_create: range-guard allocation failed");
+  }
   if (hipMalloc(&c->zero16, 256) != hipSuccess || hipMemset(c->zero16, 0, 256) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: zero buffer allocation failed");
@@ -513,6 +521,8 @@ int nic_destroy(nic_ctx* c) {
   if (c->qs) (void)hipFree(c->qs);
   if (c->zero16) (void)hipFree(c->zero16);
   if (c->wproj) (void)hipFree(c->wproj);
+  if (c->range) (void)hipFree(c->range);
+  if (c->range_host) (void)hipHostFree(c->range_host);
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
@@ -599,26 +609,33 @@ int nic_reserve(nic_ctx* c, int n, int h, int w) {
   return NIC_OK;
 }
 
-int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, float* prequant,
-               void* stream) {
-  if (!c) return fail(NIC_EINVAL, "nic_encode: NULL ctx");
-  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode: bad input shape (%d,%d,%d,3)", n, h, w);
-  if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode: encoder weights not fully set");
-  if (n == 0) return NIC_OK;  // empty batch: pointers may be NULL
-  if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode: NULL buffer");
-  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode: batch %d exceeds 21845 images per call", n);
-  DeviceGuard guard(c->device);
-  hipStream_t st = (hipStream_t)stream;
+}  // extern "C"
+
+namespace {
+
+// One encode pass: split-f16 kernels (x3, producers report to rg.flag) or exact-fp32 ones
+// (rg.gate set: a re-run that exits unless the split pass of the same epoch tripped).
+// `timed` brackets the launches with the per-layer events (the gated re-run is not timed).
+int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, float* prequant,
+                hipStream_t st, bool x3, const RangeGuard& rg, bool timed) {
   const EncGeom g = enc_geom(n, h, w);
   float* R[4];
   int rc = ensure_regions(c, g.r0, g.r123, R);
   if (rc) return rc;
   const int P = 3 * n;
+  const bool timing_on = c->timing;
+  c->timing = timing_on && timed;
+  struct Restore {
+    nic_ctx* c;
+    bool v;
+    ~Restore() { c->timing = v; }
+  } restore{c, timing_on};
 
   Conv1Args a1{};
+  a1.rg = rg;
   a1.rgb = rgb;
   a1.out = R[0];
-  a1.out_s = c->precision == NIC_PRECISION_F16X3 ? (uint16_t*)R[0] : nullptr;
+  a1.out_s = x3 ? (uint16_t*)R[0] : nullptr;
   a1.w = c->wk[L_CONV1];
   a1.bias = c->wb[L_CONV1];
   a1.P = P;
@@ -630,12 +647,17 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
   a1.pad_y = g.c1y.lo;
   a1.pad_x = g.c1x.lo;
   // f16x3: conv1 runs inside the conv2 kernel (launch_conv12_x3, timed as conv2)
-  const bool fuse12 = c->precision == NIC_PRECISION_F16X3 && conv12_fused();
+  const bool fuse12 = x3 && conv12_fused();
   if (!fuse12) TIMED(L_CONV1, launch_conv1(a1, st));
+  // the re-run's head is conv1 (it counts the trip); later layers only gate
+  RangeGuard rgl = rg;
+  rgl.trips = nullptr;
+  auto run = [&](LayerId id, const ConvArgs& a) { return x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st); };
 
   auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW, int py,
                   int px) {
     ConvArgs a{};
+    a.rg = rgl;
     a.in = in;
     a.out = out;
     a.res = res;
@@ -672,34 +694,39 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
     a2.p1x = g.c1x.lo;
     TIMED(L_CONV2, launch_conv12_x3(a2, st));
   } else {
-    TIMED(L_CONV2, run_layer(c, L_CONV2, a2, st));
+    TIMED(L_CONV2, run(L_CONV2, a2));
   }
-  TIMED(L_CONV3, run_layer(c, L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1), st));
-  TIMED(L_CONV4, run_layer(c, L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1), st));
+  TIMED(L_CONV3, run(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1)));
+  TIMED(L_CONV4, run(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1)));
   ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);
   a8.out_u8 = latent;
   a8.out_f32_latent = prequant;
-  TIMED(L_CONV8, run_layer(c, L_CONV8, a8, st));
+  TIMED(L_CONV8, run(L_CONV8, a8));
   return NIC_OK;
 }
 
-int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
-               void* stream) {
-  if (!c) return fail(NIC_EINVAL, "nic_decode: NULL ctx");
-  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_decode: bad latent shape (%d,%d,%d,96)", n, h8, w8);
-  if (!models_ready(c, 2)) return fail(NIC_ENOWEIGHTS, "nic_decode: decoder weights not fully set");
-  if (n == 0) return NIC_OK;
-  if (!latent || !rgb) return fail(NIC_EINVAL, "nic_decode: NULL buffer");
-  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_decode: batch %d exceeds 21845 images per call", n);
-  DeviceGuard guard(c->device);
-  hipStream_t st = (hipStream_t)stream;
+// One decode pass (see encode_pass).
+int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
+                hipStream_t st, bool x3, const RangeGuard& rg, bool timed) {
   const DecGeom g = dec_geom(n, h8, w8);
   float* R[4];
   int rc = ensure_regions(c, g.r0, g.r123, R);
   if (rc) return rc;
   const int P = 3 * n;
+  const bool timing_on = c->timing;
+  c->timing = timing_on && timed;
+  struct Restore {
+    nic_ctx* c;
+    bool v;
+    ~Restore() { c->timing = v; }
+  } restore{c, timing_on};
+  // the re-run's head is dconv1 (it counts the trip); later layers only gate
+  RangeGuard rgl = rg;
+  rgl.trips = nullptr;
+  auto run = [&](LayerId id, const ConvArgs& a) { return x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st); };
   auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW) {
     ConvArgs a{};
+    a.rg = rgl;
     a.in = in;
     a.out = out;
     a.res = res;
@@ -724,13 +751,14 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   };
   ConvArgs d1 = conv(L_DCONV1, nullptr, R[1], nullptr, h8, w8, 2 * h8, 2 * w8);
   d1.in_u8 = latent;
-  TIMED(L_DCONV1, run_layer(c, L_DCONV1, d1, st));
+  d1.rg = rg;
+  TIMED(L_DCONV1, run(L_DCONV1, d1));
   const int h2 = 2 * h8, w2 = 2 * w8;
-  TIMED(L_DCONV5, run_layer(c, L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2), st));
-  TIMED(L_DCONV6, run_layer(c, L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2), st));
+  TIMED(L_DCONV5, run(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2)));
+  TIMED(L_DCONV6, run(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2)));
   ConvArgs d7 = conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2);
   // f16x3: dconv7 writes dconv8's per-pixel tap projections (100 B / pixel instead of 256)
-  const bool fuse78 = c->precision == NIC_PRECISION_F16X3 && dconv78_fused();
+  const bool fuse78 = x3 && dconv78_fused();
   if (fuse78) {
     d7.proj = R[0];
     d7.proj_w = c->wproj;
@@ -738,9 +766,10 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
     d7.proj_scale[1] = c->wscale[L_DCONV8][1];
     TIMED(L_DCONV7, launch_dconv7_proj_x3(d7, st));
   } else {
-    TIMED(L_DCONV7, run_layer(c, L_DCONV7, d7, st));
+    TIMED(L_DCONV7, run(L_DCONV7, d7));
   }
   Dconv8Args a8{};
+  a8.rg = rgl;
   a8.in = R[0];
   a8.in_s = (const uint16_t*)R[0];
   a8.zero16 = c->zero16;
@@ -760,9 +789,73 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
     a8.tiles_x7 = (w2 + 7) / 8;
     TIMED(L_DCONV8, launch_dconv8_gather(a8, st));
   } else {
-    TIMED(L_DCONV8, c->precision == NIC_PRECISION_F16X3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
+    TIMED(L_DCONV8, x3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
   }
   return NIC_OK;
+}
+
+// The f16 range guard around a split-f16 pass (nic.h, NIC_RANGE_*): the pass's producers
+// report to the ctx's flag word under a fresh epoch; then either the exact-fp32 re-run is
+// queued behind it, gated on that epoch (FALLBACK: stream-ordered, no host sync), or the
+// stream is synchronised and a tripped pass returns NIC_ERANGE (ERROR).
+template <class Pass>
+int guarded(nic_ctx* c, hipStream_t st, const char* what, Pass pass) {
+  if (c->precision != NIC_PRECISION_F16X3) return pass(false, RangeGuard{}, true);
+  if (++c->epoch <= 0) c->epoch = 1;  // the flag word starts at 0: never a live epoch
+  RangeGuard prod{};
+  prod.flag = c->range;
+  prod.epoch = c->epoch;
+  int rc = pass(true, prod, true);
+  if (rc) return rc;
+  if (c->range_policy == NIC_RANGE_FALLBACK) {
+    RangeGuard gate{};
+    gate.gate = c->range;
+    gate.trips = c->range + 1;
+    gate.epoch = c->epoch;
+    return pass(false, gate, false);
+  }
+  HIP_TRY(hipMemcpyAsync(c->range_host, c->range, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (*c->range_host == c->epoch) {
+    ++c->error_trips;
+    return fail(NIC_ERANGE, "%s: an activation reached the f16 limit of the split-f16 pass (|x| >= 65504); "
+                "outputs are undefined (use NIC_RANGE_FALLBACK or NIC_PRECISION_FP32)", what);
+  }
+  return NIC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, float* prequant,
+               void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_encode: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode: encoder weights not fully set");
+  if (n == 0) return NIC_OK;  // empty batch: pointers may be NULL
+  if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  return guarded(c, st, "nic_encode", [&](bool x3, const RangeGuard& rg, bool timed) {
+    return encode_pass(c, rgb, n, h, w, latent, prequant, st, x3, rg, timed);
+  });
+}
+
+int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
+               void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_decode: NULL ctx");
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_decode: bad latent shape (%d,%d,%d,96)", n, h8, w8);
+  if (!models_ready(c, 2)) return fail(NIC_ENOWEIGHTS, "nic_decode: decoder weights not fully set");
+  if (n == 0) return NIC_OK;
+  if (!latent || !rgb) return fail(NIC_EINVAL, "nic_decode: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_decode: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  return guarded(c, st, "nic_decode", [&](bool x3, const RangeGuard& rg, bool timed) {
+    return decode_pass(c, latent, n, h8, w8, rgb, rgb_f32, st, x3, rg, timed);
+  });
 }
 
 int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,
@@ -790,9 +883,13 @@ int nic_ms_ssim(nic_ctx* c, const uint8_t* a, const uint8_t* b, int n, int h, in
                 float* per_scale, void* stream) {
   if (!c) return fail(NIC_EINVAL, "nic_ms_ssim: NULL ctx");
   if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_ms_ssim: bad image shape (%d,%d,%d,3)", n, h, w);
-  if (h < 176 || w < 176)
-    return fail(NIC_ESHAPE, "nic_ms_ssim: images must be at least 176x176 (5 scales of an 11x11 window), got %dx%d",
-                h, w);
+  {  // tf.image.ssim_multiscale: every scale (ceil halving) holds the 11 x 11 window
+    int sh = h, sw = w;
+    for (int k = 0; k < kSsimScales; ++k, sh = (sh + 1) / 2, sw = (sw + 1) / 2)
+      if (sh < 11 || sw < 11)
+        return fail(NIC_ESHAPE, "nic_ms_ssim: scale %d of a %dx%d image is %dx%d, smaller than the 11x11 window "
+                    "(H, W >= 161)", k, h, w, sh, sw);
+  }
   if (n == 0) return NIC_OK;
   if (!a || !b || !ms_ssim) return fail(NIC_EINVAL, "nic_ms_ssim: NULL argument");
   if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_ms_ssim: batch %d too large", n);
@@ -849,6 +946,24 @@ int nic_set_precision(nic_ctx* c, int mode) {
 int nic_get_precision(nic_ctx* c, int* mode) {
   if (!c || !mode) return fail(NIC_EINVAL, "nic_get_precision: NULL argument");
   *mode = c->precision;
+  return NIC_OK;
+}
+
+int nic_set_range_policy(nic_ctx* c, int policy) {
+  if (!c) return fail(NIC_EINVAL, "nic_set_range_policy: NULL ctx");
+  if (policy != NIC_RANGE_FALLBACK && policy != NIC_RANGE_ERROR)
+    return fail(NIC_EINVAL, "nic_set_range_policy: unknown policy %d", policy);
+  c->range_policy = policy;
+  return NIC_OK;
+}
+
+int nic_range_trips(nic_ctx* c, int64_t* passes) {
+  if (!c || !passes) return fail(NIC_EINVAL, "nic_range_trips: NULL argument");
+  DeviceGuard guard(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  int reruns = 0;
+  HIP_TRY(hipMemcpy(&reruns, c->range + 1, sizeof(int), hipMemcpyDeviceToHost));
+  *passes = (int64_t)reruns + c->error_trips;
   return NIC_OK;
 }
 

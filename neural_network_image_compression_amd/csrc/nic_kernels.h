@@ -17,7 +17,19 @@ enum LayerId {
   L_COUNT
 };
 
+// f16 range guard of the split format: a split-f16 producer whose fp32 value reaches the
+// f16 limit (|v| >= 65504, or non-finite) stores `epoch` into *flag (one word per ctx); the
+// exact-fp32 re-run of the pass is gated on *gate == epoch (fp32 kernels exit otherwise).
+constexpr float kF16Limit = 65504.0f;
+struct RangeGuard {
+  int* flag = nullptr;        // f16x3 producers: set to epoch on overflow
+  const int* gate = nullptr;  // fp32 kernels: run only when *gate == epoch
+  int* trips = nullptr;       // head kernel of a gated re-run: +1 when it runs
+  int epoch = 0;
+};
+
 struct ConvArgs {
+  RangeGuard rg;
   const float* in;        // [P][H][W][Cin] fp32 (IN_F32)
   const uint8_t* in_u8;   // [N][H][W][96] latent (IN_U8_LATENT)
   float* out;             // [P][OH][OW][Cout] fp32 (OUT_F32)
@@ -57,15 +69,17 @@ struct ConvArgs {
 };
 
 struct Conv1Args {
+  RangeGuard rg;
   const uint8_t* rgb;  // [N][H][W][3]
   float* out;          // [P][OH][OW][32] fp32 (exact mode)
   uint16_t* out_s;     // [P][OH][OW][2][32] split f16 (f16x3 mode), used when non-null
   const float* w;      // [2][26][32]
   const float* bias;   // [2][32]
-  int P, nimg, H, W, OH, OW, pad_y, pad_x, tiles_x;
+  int P, nimg, H, W, OH, OW, pad_y, pad_x, tiles_x, tiles_y;
 };
 
 struct Dconv8Args {
+  RangeGuard rg;
   const float* in;      // [P][H][W][64] fp32 (exact mode)
   const uint16_t* in_s; // [P][H][W][2][64] split f16 (f16x3 mode)
   const char* zero16;   // DMA padding source
@@ -75,7 +89,7 @@ struct Dconv8Args {
   const uint16_t* wx;   // f16x3 path: [2][9 nbr][2 chunk][hi,lo][64 lanes][8] MFMA A fragments
   float wscale[2];      // f16x3 path: 2^-k per model
   const float* bias;    // [2]
-  int nimg, H, W, tiles_x;
+  int nimg, H, W, tiles_x, tiles_y;
   int strips, nseg, seg_rows;  // strip-walk kernel: column strips, row segments
   const float* proj;           // gather kernel: dconv7's projections (ConvArgs::proj layout)
   int tiles_y7, tiles_x7;      // gather kernel: dconv7's 8x8 tile grid over its coarse input

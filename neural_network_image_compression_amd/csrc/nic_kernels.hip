@@ -99,6 +99,24 @@ __device__ __forceinline__ uint8_t quant255(float v) {
   // np.round(v * 255).astype(np.uint8) for v in [0, 1]: fp32 multiply, round half to even
   return (uint8_t)(int)rintf(__fmul_rn(v, 255.0f));
 }
+// f16 range guard (RangeGuard, nic_kernels.h).  Every split-f16 producer keeps a running
+// max of |v| over the values it splits (one v_max_f32 per value) and reports once per lane
+// at the end: a value at or beyond the f16 limit would split into +-inf.  NaN needs an inf
+// first (finite operands; products bounded by the weight pre-scale), so the max catches it.
+__device__ __forceinline__ void range_track(float& m, const f32x4& v) {
+  m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+}
+__device__ __forceinline__ void range_report(const RangeGuard& rg, float m) {
+  if (!(m < kF16Limit) && rg.flag) atomicExch(rg.flag, rg.epoch);  // vector atomic, rare
+}
+// exact-fp32 re-run of a pass: the kernel does nothing unless the f16x3 pass it backs up
+// (same epoch) tripped the guard
+__device__ __forceinline__ bool range_gated_off(const RangeGuard& rg) {
+  if (rg.gate && *(volatile const int*)rg.gate != rg.epoch) return true;
+  if (rg.trips && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(rg.trips, 1);  // a re-run starts
+  return false;
+}
+
 // ((t0*k0 + t1*k1) + t2*k2), every op rounded (utils.py:64-68)
 __device__ __forceinline__ float project(const float* k, float t0, float t1, float t2) {
   return __fadd_rn(__fadd_rn(__fmul_rn(t0, k[0]), __fmul_rn(t1, k[1])), __fmul_rn(t2, k[2]));
@@ -215,9 +233,14 @@ template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
   __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-
-  const int p = blockIdx.y;
-  const int tile = blockIdx.x;
+  if (range_gated_off(a.rg)) return;
+  // grid-stride over (plane, tile) jobs: a capped grid, so that a gated launch that has
+  // nothing to do (the f16x3 pass it backs up stayed in range) costs one small dispatch
+  const int per_plane = a.tiles_y * a.tiles_x;
+  for (int job = blockIdx.x; job < per_plane * a.P; job += gridDim.x) {
+  __syncthreads();  // every wave is done with the previous job's LDS
+  const int p = job / per_plane;
+  const int tile = job - p * per_plane;
   const int tyi = tile / a.tiles_x;
   const int t0y = tyi * TH, t0x = (tile - tyi * a.tiles_x) * TW;
   const int model = p >= a.nimg ? 1 : 0;
@@ -298,7 +321,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
               lds[((((wk - 1) * WM * WN + grp) * G::MTW + i) * G::NTW + j) * 1024 + r * 64 + lane] = acc[i][j][r];
       }
       __syncthreads();
-      if (wk > 0) return;
+      if (wk > 0) continue;  // to the next job's barrier
 #pragma unroll
       for (int k = 1; k < WK; ++k)
 #pragma unroll
@@ -382,6 +405,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
       tap_base += ny * nx;
     }
   }
+  }  // job
 }
 
 
@@ -705,7 +729,7 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
 // BiasAdd -> leaky (-> + residual | -> clip, round(x*255) into the latent layout).
 template <int COUT, int OUT_MODE, bool RESID>
 __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, const f32x16& acc, int oy, int ox,
-                                             float scale, const f32x4 (&b)[4]) {
+                                             float scale, const f32x4 (&b)[4], float& rmax) {
   const bool inside = oy < a.OH && ox < a.OW;
   const int half = (threadIdx.x >> 5) & 1;
   const size_t pix = ((size_t)p * (inside ? a.OH : 1) + (inside ? oy : 0)) * (inside ? a.OW : 1) + (inside ? ox : 0);
@@ -742,6 +766,10 @@ __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, c
           v[g][c] = __fadd_rn(v[g][c], __fadd_rn((float)h0[c], (float)l0[c]));
           v[g + 1][c] = __fadd_rn(v[g + 1][c], __fadd_rn((float)h1[c], (float)l1[c]));
         }
+      }
+      if (inside) {
+        range_track(rmax, v[g]);
+        range_track(rmax, v[g + 1]);
       }
       f16x4 h0, l0, h1, l1;
       split4(v[g], h0, l0);
@@ -869,6 +897,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   load_a_x3<MTW, CIN>(ahi, alo, lds, a_off, tap_off(t_begin));
 
   f32x16 acc[MTW][NTW];
+  float rmax = 0.f;  // range guard of the split output
   auto zero_acc = [&]() {
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
@@ -935,7 +964,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
         store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale,
-                                            bias4[j]);
+                                            bias4[j], rmax);
     NIC_STAMP(3);
   } else {
     static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
@@ -950,10 +979,11 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
           store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
-                                              2 * (t0x + mx[i]) + px, scale, bias4[j]);
+                                              2 * (t0x + mx[i]) + px, scale, bias4[j], rmax);
     }
     NIC_STAMP(3);
   }
+  range_report(a.rg, rmax);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1162,6 +1192,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   // 16w + 8 (g >> 1) .. +7
   const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
   int ep_p = 0, ep_y = 0, ep_x = 0;  // tile whose epilogue is pending
+  float rmax = 0.f;                  // range guard of the split output
 #ifdef NIC_STAMPS
   unsigned long long s_wait = 0, s_epi = 0, s_mfma = 0, s_t0, s_t1, s_t2;
   const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
@@ -1193,6 +1224,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = __fadd_rn(v[r], __fadd_rn((float)rh[r], (float)rl[r]));
         }
+        if (y < a.H && x < a.W) range_track(rmax, v);
         f16x4 hi, lo;
         split4(v, hi, lo);
         u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
@@ -1297,6 +1329,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     }
     __builtin_amdgcn_s_setprio(0);
   }
+  range_report(a.rg, rmax);
 #ifdef NIC_STAMPS
   if (threadIdx.x == 0) {
     unsigned long long* o = g_stamps + blockIdx.x * 8;
@@ -1476,6 +1509,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   f32x4 acc[MT];
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
   int ep_p = 0, ep_y = 0, ep_x = 0;
+  float rmax = 0.f;  // range guard of the split outputs (conv2's, and conv1's into the halo)
   if constexpr (!FUSE1)
     if (ntile > 0) issue(0);
 #ifdef NIC_STAMPS
@@ -1514,6 +1548,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
           if constexpr (OUT_MODE == OUT_SPLIT) {
+            if (oy < a.OH && ox < a.OW) range_track(rmax, v);
             f16x4 hi, lo;
             split4(v, hi, lo);
             const u32x4 q = swap16_pair(hi, lo);
@@ -1611,6 +1646,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
           f32x4 v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
+          range_track(rmax, v);
           f16x4 hi, lo;
           split4(v, hi, lo);
           if (qv) {
@@ -1662,6 +1698,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
     }
   }
+  range_report(a.rg, rmax);
 #ifdef NIC_STAMPS
   if (lane == 0) {
     unsigned long long* o = g_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
@@ -1729,11 +1766,16 @@ constexpr int C1_PS = 40;
 
 __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
   __shared__ float plane[C1_HH * C1_PS];
-  const int p = blockIdx.y;
+  if (range_gated_off(a.rg)) return;
+  float rmax = 0.f;  // range guard of the split output
+  const int per_plane = a.tiles_y * a.tiles_x;
+  for (int job = blockIdx.x; job < per_plane * a.P; job += gridDim.x) {  // capped grid, as conv_mfma
+  __syncthreads();  // the previous job's plane reads are done
+  const int p = job / per_plane, tile = job - p * per_plane;
   const int n = p % a.nimg, type = p / a.nimg;
   const int model = type > 0 ? 1 : 0;
-  const int tyi = blockIdx.x / a.tiles_x;
-  const int t0y = tyi * C1_T, t0x = (blockIdx.x - tyi * a.tiles_x) * C1_T;
+  const int tyi = tile / a.tiles_x;
+  const int t0y = tyi * C1_T, t0x = (tile - tyi * a.tiles_x) * C1_T;
   const int gy0 = t0y * 2 - a.pad_y, gx0 = t0x * 2 - a.pad_x;
   const uint8_t* img = a.rgb + (size_t)n * a.H * a.W * 3;
   const float* k = c_ycbcr + type * 3;
@@ -1802,6 +1844,10 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
     if (a.out_s) {  // split format for the f16x3 conv2: 16-B stores after lane-half swaps
 #pragma unroll
       for (int g = 0; g < 4; g += 2) {
+        if (inside) {
+          range_track(rmax, v[g]);
+          range_track(rmax, v[g + 1]);
+        }
         f16x4 h0, l0, h1, l1;
         split4(v[g], h0, l0);
         split4(v[g + 1], h1, l1);
@@ -1818,6 +1864,8 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
       for (int g = 0; g < 4; ++g) *(f32x4*)(a.out + pix * 32 + 8 * g + 4 * half) = v[g];
     }
   }
+  }  // job
+  range_report(a.rg, rmax);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1889,9 +1937,12 @@ __device__ __forceinline__ void d8_store_rgb(const Dconv8Args& a, int n, int my,
 
 __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HW * D8_PS];
-  const int n = blockIdx.y;
-  const int tyi = blockIdx.x / a.tiles_x;
-  const int t0y = tyi * D8_TH, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_TW;
+  if (range_gated_off(a.rg)) return;
+  const int per_img = a.tiles_y * a.tiles_x;
+  for (int job = blockIdx.x; job < per_img * a.nimg; job += gridDim.x) {  // capped grid, as conv_mfma
+  const int n = job / per_img, tile = job - n * per_img;
+  const int tyi = tile / a.tiles_x;
+  const int t0y = tyi * D8_TH, t0x = (tile - tyi * a.tiles_x) * D8_TW;
   const int ty = threadIdx.x / D8_TW, tx = threadIdx.x % D8_TW;
   float outv[3][4];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1951,8 +2002,8 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   }
 
   const int my = t0y + ty, mx = t0x + tx;
-  if (my >= a.H || mx >= a.W) return;
-  d8_store_rgb(a, n, my, mx, outv);
+  if (my < a.H && mx < a.W) d8_store_rgb(a, n, my, mx, outv);
+  }  // job (the next job's first step barrier orders the halo reuse)
 }
 
 // ------------------------------------------------------------------------------------
@@ -2535,11 +2586,14 @@ template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int
           int OUT_MODE, bool RESID>
 static hipError_t launch_conv(ConvArgs a, hipStream_t st) {
   const int gy = TR ? a.H : a.OH, gx = TR ? a.W : a.OW;  // tile grid over coarse / output coords
-  const int tiles_y = (gy + TH - 1) / TH;
+  a.tiles_y = (gy + TH - 1) / TH;
   a.tiles_x = (gx + TW - 1) / TW;
-  dim3 grid(tiles_y * a.tiles_x, a.P);
-  hipLaunchKernelGGL((conv_mfma_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>), grid,
-                     dim3(256), 0, st, a);
+  const long long jobs = (long long)a.tiles_y * a.tiles_x * a.P;
+  if (jobs == 0) return hipSuccess;
+  if (jobs > INT32_MAX) return hipErrorInvalidValue;
+  const int grid = (int)std::min<long long>(jobs, 8LL * device_cus());
+  hipLaunchKernelGGL((conv_mfma_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>),
+                     dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2722,16 +2776,24 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_conv1(Conv1Args a, hipStream_t st) {
-  const int tiles_y = (a.OH + C1_T - 1) / C1_T;
+  a.tiles_y = (a.OH + C1_T - 1) / C1_T;
   a.tiles_x = (a.OW + C1_T - 1) / C1_T;
-  hipLaunchKernelGGL(conv1_colour_kernel, dim3(tiles_y * a.tiles_x, a.P), dim3(256), 0, st, a);
+  const long long jobs = (long long)a.tiles_y * a.tiles_x * a.P;
+  if (jobs == 0) return hipSuccess;
+  if (jobs > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv1_colour_kernel, dim3((int)std::min<long long>(jobs, 8LL * device_cus())), dim3(256), 0,
+                     st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
-  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
+  a.tiles_y = (a.H + D8_TH - 1) / D8_TH;
   a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
-  hipLaunchKernelGGL(dconv8_colour_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  const long long jobs = (long long)a.tiles_y * a.tiles_x * a.nimg;
+  if (jobs == 0) return hipSuccess;
+  if (jobs > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dconv8_colour_kernel, dim3((int)std::min<long long>(jobs, 8LL * device_cus())), dim3(256), 0,
+                     st, a);
   return hipGetLastError();
 }
 

@@ -67,8 +67,10 @@ def gather_rows(local, n_total: int, dist, dst: Optional[int] = 0):
     """Gather per-rank shards (leading dim = shard rows, from :func:`shard_range`) into the
     full ``n_total``-row tensor on ``dst`` (or on every rank when dst is None).
 
-    Uses one all_gather of equal-sized padded blocks (RCCL/gloo friendly), then drops the
-    padding.  Returns None on non-destination ranks.
+    Equal-sized padded blocks (RCCL/gloo friendly), padding dropped afterwards.  With a
+    single destination this is one ``gather``: only ``dst`` receives the world's blocks (an
+    all_gather would move world-fold the bytes over xGMI, every other rank discarding them);
+    ``dst=None`` is one ``all_gather``.  Returns None on non-destination ranks.
     """
     import torch
 
@@ -79,10 +81,14 @@ def gather_rows(local, n_total: int, dist, dst: Optional[int] = 0):
         raise ValueError(f"rank {rank}: shard has {local.shape[0]} rows, expected {hi - lo}")
     block = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     block[: hi - lo] = local
-    blocks = [torch.empty_like(block) for _ in range(world)]
-    dist.all_gather(blocks, block)
-    if dst is not None and rank != dst:
-        return None
+    if dst is None:
+        blocks = [torch.empty_like(block) for _ in range(world)]
+        dist.all_gather(blocks, block)
+    else:
+        blocks = [torch.empty_like(block) for _ in range(world)] if rank == dst else None
+        dist.gather(block, gather_list=blocks, dst=dst)
+        if rank != dst:
+            return None
     parts = []
     for r in range(world):
         a, b = shard_range(n_total, world, r)

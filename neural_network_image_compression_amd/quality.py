@@ -17,6 +17,20 @@ from .bitstream import read_dataset
 from .codec import Codec
 
 
+MS_SSIM_SCALES = 5
+SSIM_FILTER = 11
+
+
+def ms_ssim_supported(h: int, w: int) -> bool:
+    """tf.image.ssim_multiscale's shape rule: each of the 5 scales (odd sizes SYMMETRIC-padded,
+    then halved: ceil(n / 2)) must hold the 11 x 11 window -- H, W >= 161."""
+    for _ in range(MS_SSIM_SCALES - 1):
+        if min(h, w) < SSIM_FILTER:
+            return False
+        h, w = -(-h // 2), -(-w // 2)
+    return min(h, w) >= SSIM_FILTER
+
+
 def _dev(codec: Codec, a: np.ndarray):
     import torch
 

@@ -21,6 +21,7 @@ import numpy as np
 
 from .bitstream import png_bytes
 from .codec import Codec
+from .quality import ms_ssim_supported
 
 
 def tile_patches(x: np.ndarray, tile: int) -> np.ndarray:
@@ -68,7 +69,7 @@ def rd_point(codec: Codec, images: np.ndarray, tile: Optional[int] = None, png: 
     out: Dict[str, object] = {"images": n, "size": [h, w], "tile": tile,
                               "bpp_entropy": sym_bits / (h * w),
                               "psnr_db": codec.psnr(x_d, rec_d, per_image=True)}
-    if min(h, w) >= 176:
+    if ms_ssim_supported(h, w):
         out["ms_ssim"] = codec.ms_ssim(x_d, rec_d).cpu().numpy().astype(np.float64)
     if png:
         from concurrent.futures import ThreadPoolExecutor

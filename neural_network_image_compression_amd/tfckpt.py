@@ -11,8 +11,14 @@ TensorFlow is not installable here, so this module restates the published format
 (``tensorflow/core/protobuf/tensor_bundle.proto``, ``core/lib/io/table_builder.cc`` /
 ``format.cc``: blocks of prefix-compressed entries + restart array + 5-byte trailer,
 an index block of block handles, a 48-byte footer with magic 0xdb4775248b80fb57; masked
-CRC32C).  Parity against checkpoints written by TF itself is **unpinned**: none ship
-with the reference; the tests round-trip through :func:`write_bundle`.
+CRC32C).  Bundles written here also carry the ``_CHECKPOINTABLE_OBJECT_GRAPH`` entry
+(a scalar DT_STRING holding a serialized ``TrackableObjectGraph``,
+``tensorflow/core/protobuf/trackable_object_graph.proto``) that TF2's object-based restore
+(``Model.load_weights``, utils.py:26-28) walks to match checkpoint keys to variables:
+root -> one child per layer attribute -> ``kernel`` / ``bias`` -> a ``VARIABLE_VALUE``
+attribute with its checkpoint key.  Parity against checkpoints written, or read, by TF
+itself is **unpinned**: none ship with the reference and TF is absent; the tests
+round-trip through :func:`write_bundle` and decode the object graph back.
 """
 from __future__ import annotations
 
@@ -32,6 +38,8 @@ DTYPES = {1: np.float32, 2: np.float64, 3: np.int32, 4: np.uint8, 5: np.int16, 6
 DTYPE_IDS = {np.dtype(v): k for k, v in DTYPES.items()}
 
 VARIABLE_SUFFIX = "/.ATTRIBUTES/VARIABLE_VALUE"
+OBJECT_GRAPH_KEY = "_CHECKPOINTABLE_OBJECT_GRAPH"
+DT_STRING = 7
 
 
 # --- CRC32C (Castagnoli), masked as LevelDB / TF do ------------------------------------
@@ -149,6 +157,86 @@ def encode_entry(dtype: int, shape: Tuple[int, ...], offset: int, size: int, crc
     out += _enc_field(5, 0, _enc_varint(size))
     out += _enc_field(6, 5, struct.pack("<I", crc))
     return out
+
+
+def _enc_bytes(f: int, b: bytes) -> bytes:
+    return _enc_field(f, 2, _enc_varint(len(b)) + b)
+
+
+def encode_object_graph(variable_keys: Iterable[str], scope: str = "") -> bytes:
+    """TrackableObjectGraph of a subclassed Keras model whose attribute layers own the
+    variables ``<layer>/<var>`` (keys ``<layer>/<var>/.ATTRIBUTES/VARIABLE_VALUE``):
+    nodes = [root, layer..., variable...]; TrackableObject: children = 1 (ObjectReference:
+    node_id = 1, local_name = 2), attributes = 2 (SerializedTensor: name = 1, full_name = 2,
+    checkpoint_key = 3).  ``scope`` prefixes the informational full names."""
+    names = sorted(k[:-len(VARIABLE_SUFFIX)] if k.endswith(VARIABLE_SUFFIX) else k for k in variable_keys)
+    layers: Dict[str, List[str]] = {}
+    for n in names:
+        layer, var = n.split("/")
+        layers.setdefault(layer, []).append(var)
+    layer_ids = {layer: 1 + i for i, layer in enumerate(layers)}
+    var_ids, nid = {}, 1 + len(layers)
+    for layer, vars_ in layers.items():
+        for v in vars_:
+            var_ids[(layer, v)] = nid
+            nid += 1
+
+    def ref(node_id: int, local: str) -> bytes:
+        return _enc_bytes(1, _enc_field(1, 0, _enc_varint(node_id)) + _enc_bytes(2, local.encode()))
+
+    nodes = [b"".join(ref(layer_ids[layer], layer) for layer in layers)]
+    for layer, vars_ in layers.items():
+        nodes.append(b"".join(ref(var_ids[(layer, v)], v) for v in vars_))
+    for layer, vars_ in layers.items():
+        for v in vars_:
+            full = "/".join(p for p in (scope, layer, v) if p)
+            tensor = (_enc_bytes(1, b"VARIABLE_VALUE") + _enc_bytes(2, full.encode()) +
+                      _enc_bytes(3, f"{layer}/{v}{VARIABLE_SUFFIX}".encode()))
+            nodes.append(_enc_bytes(2, tensor))
+    return b"".join(_enc_bytes(1, n) for n in nodes)
+
+
+def decode_object_graph(buf: bytes) -> List[dict]:
+    """Inverse of :func:`encode_object_graph` (any TrackableObjectGraph): per node
+    {"children": [(node_id, local_name)], "attributes": [(name, full_name, checkpoint_key)]}."""
+    nodes = []
+    for f, _, node in _proto_fields(buf):
+        if f != 1:
+            continue
+        children, attrs = [], []
+        for f2, _, v in _proto_fields(node):
+            if f2 == 1:
+                d = {k: x for k, _, x in _proto_fields(v)}
+                children.append((d.get(1, 0), d.get(2, b"").decode()))
+            elif f2 == 2:
+                d = {k: x for k, _, x in _proto_fields(v)}
+                attrs.append(tuple(d.get(k, b"").decode() for k in (1, 2, 3)))
+        nodes.append({"children": children, "attributes": attrs})
+    return nodes
+
+
+def _string_tensor_bytes(elems: List[bytes]) -> Tuple[bytes, int]:
+    """TF's WriteStringTensor (tensor_bundle.cc): varint64 lengths, the masked CRC32C of the
+    lengths taken as uint32s, then the bytes; returns (blob, crc32c over all of it as TF
+    extends it: the uint32 lengths, the length checksum, the string bytes)."""
+    lengths, crc = b"", 0
+    for e in elems:
+        lengths += _enc_varint(len(e))
+        crc = crc32c(struct.pack("<I", len(e)), crc)
+    lcrc = struct.pack("<I", mask_crc(crc))
+    crc = crc32c(lcrc, crc)
+    for e in elems:
+        crc = crc32c(e, crc)
+    return lengths + lcrc + b"".join(elems), crc
+
+
+def _read_string_scalar(blob: bytes, verify: bool, key: str) -> bytes:
+    n, pos = _varint(blob, 0)
+    if verify:
+        crc = crc32c(struct.pack("<I", n))
+        if struct.unpack_from("<I", blob, pos)[0] != mask_crc(crc):
+            raise ValueError(f"string tensor {key!r}: length checksum mismatch")
+    return bytes(blob[pos + 4:pos + 4 + n])
 
 
 # --- LevelDB table format ---------------------------------------------------------------
@@ -276,8 +364,30 @@ def read_bundle(prefix: str, verify: bool = True) -> Dict[str, np.ndarray]:
     return out
 
 
-def write_bundle(prefix: str, tensors: Dict[str, np.ndarray]) -> List[str]:
-    """Single-shard little-endian bundle of ``tensors`` (keys written in sorted order)."""
+def read_object_graph(prefix: str, verify: bool = True) -> List[dict]:
+    """The decoded ``_CHECKPOINTABLE_OBJECT_GRAPH`` of a bundle (KeyError if it has none)."""
+    table = read_table(prefix + ".index", verify)
+    header = table.get("", b"")
+    num_shards = next((v for f, _, v in _proto_fields(header) if f == 1), 1)
+    e = parse_entry(table[OBJECT_GRAPH_KEY])
+    if e["dtype"] != DT_STRING or e["shape"]:
+        raise ValueError(f"{prefix}: {OBJECT_GRAPH_KEY} is not a scalar DT_STRING")
+    with open(f"{prefix}.data-{e['shard_id']:05d}-of-{num_shards:05d}", "rb") as f:
+        f.seek(e["offset"])
+        blob = f.read(e["size"])
+    payload = _read_string_scalar(blob, verify, OBJECT_GRAPH_KEY)
+    if verify and e["crc32c"] is not None:
+        # the entry CRC of a string tensor extends over the lengths as uint32s, not their varints
+        rebuilt, crc = _string_tensor_bytes([payload])
+        if rebuilt != blob or mask_crc(crc) != e["crc32c"]:
+            raise ValueError(f"{prefix}: {OBJECT_GRAPH_KEY} fails its CRC32C")
+    return decode_object_graph(payload)
+
+
+def write_bundle(prefix: str, tensors: Dict[str, np.ndarray], object_graph: bytes = None) -> List[str]:
+    """Single-shard little-endian bundle of ``tensors`` (keys written in sorted order), plus
+    ``object_graph`` (a serialized TrackableObjectGraph) as the scalar DT_STRING entry
+    ``_CHECKPOINTABLE_OBJECT_GRAPH`` when given."""
     d = os.path.dirname(prefix)
     if d:
         os.makedirs(d, exist_ok=True)
@@ -290,6 +400,10 @@ def write_bundle(prefix: str, tensors: Dict[str, np.ndarray]) -> List[str]:
             raise TypeError(f"write_bundle: dtype {a.dtype} of {key!r} not supported")
         blob = a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes()
         entries[key] = encode_entry(DTYPE_IDS[a.dtype], a.shape, len(data), len(blob), mask_crc(crc32c(blob)))
+        data.extend(blob)
+    if object_graph is not None:
+        blob, crc = _string_tensor_bytes([object_graph])
+        entries[OBJECT_GRAPH_KEY] = encode_entry(DT_STRING, (), len(data), len(blob), mask_crc(crc))
         data.extend(blob)
     write_table(prefix + ".index", entries)
     dpath = prefix + ".data-00000-of-00001"

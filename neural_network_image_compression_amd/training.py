@@ -174,8 +174,28 @@ class Entropynet:
         return x.clamp(0, 8)
 
 
+KERAS_ADAM_EPS = 1e-7
+ADAM_BETA2 = 0.999
+
+
+def keras_adam_eps(step: int, eps: float = KERAS_ADAM_EPS, beta2: float = ADAM_BETA2) -> float:
+    """torch.optim.Adam's eps that reproduces tf.keras Adam's update at (1-based) ``step``.
+
+    Keras computes lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t) and theta -= lr_t * m / (sqrt(v) + eps)
+    (epsilon-hat, added to the uncorrected sqrt(v)); torch adds eps to sqrt(v_hat) =
+    sqrt(v) / sqrt(1 - b2^t).  The two agree when torch's eps = eps / sqrt(1 - b2^t)
+    (about 32x the Keras value at step 1, tending to it)."""
+    return eps / float(np.sqrt(1.0 - beta2 ** step))
+
+
 class Training:
-    """training.py:44-172."""
+    """training.py:44-172.
+
+    Parity notes (unpinned: no TF here): the optimiser follows Keras' Adam exactly
+    (:func:`keras_adam_eps`); the entropy net's bpp target uses Pillow's PNG encoder
+    (``png_bpp_planes``, the one the reference's own ``save_img`` uses, utils.py:85-87)
+    where the reference's ``get_bpp`` calls ``tf.image.encode_png`` (training.py:12), so
+    the target's byte counts may differ from TF's by the two zlib front ends."""
 
     def __init__(self, device: str = "cuda", weights: Optional[W.Weights] = None, seed: int = 0,
                  checkpoint_dir: str = "../checkpoints/"):
@@ -205,8 +225,8 @@ class Training:
         if self.entropy_model is None:
             self.entropy_model = Entropynet((-(-hw[0] // 8), -(-hw[1] // 8)), self.device, self.seed)
         if self._opt is None:
-            # tf.keras.optimizers.Adam(1e-4): beta 0.9 / 0.999, epsilon 1e-7
-            mk = lambda ps: torch.optim.Adam(ps, lr=1e-4, betas=(0.9, 0.999), eps=1e-7)  # noqa: E731
+            # tf.keras.optimizers.Adam(1e-4): beta 0.9 / 0.999, epsilon 1e-7 (see keras_adam_eps)
+            mk = lambda ps: torch.optim.Adam(ps, lr=1e-4, betas=(0.9, 0.999), eps=KERAS_ADAM_EPS)  # noqa: E731
             self._opt = (mk(self._variables("Y")), mk(self._variables("CbCr")), mk(self.entropy_model.parameters()))
 
     def train_step(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
@@ -253,6 +273,9 @@ class Training:
                                    (opt_e, ent_params, ge)):
             for prm, g in zip(params, grads):
                 prm.grad = g
+            for group in opt.param_groups:  # Keras' epsilon-hat at this step (keras_adam_eps)
+                st = opt.state.get(group["params"][0], {}).get("step", 0)
+                group["eps"] = keras_adam_eps(int(st) + 1)
             opt.step()
             opt.zero_grad(set_to_none=True)
         cb, cr = torch.split(ssim1_each.detach(), b)

@@ -209,14 +209,18 @@ def save(w: Weights, path_prefix: str, kind: str) -> List[str]:
 def save_tf(w: Weights, path_prefix: str, kind: str) -> List[str]:
     """The reference's own format: ``Model.save_weights(path_prefix + name)`` for name in
     Y, CbCr (training.py:167-170), i.e. TF object-based tensor bundles keyed
-    ``<layer>/<kernel|bias>/.ATTRIBUTES/VARIABLE_VALUE`` (see tfckpt.py)."""
+    ``<layer>/<kernel|bias>/.ATTRIBUTES/VARIABLE_VALUE`` plus the TrackableObjectGraph that
+    object-based restore walks (see tfckpt.py; loading these files with TF's own
+    ``load_weights`` is unpinned: TF is not available here)."""
     from . import tfckpt
 
     paths = []
-    for name, sub in split_models(w, kind).items():
+    for i, (name, sub) in enumerate(split_models(w, kind).items()):
         m = kind + name + "/"
         tensors = {k[len(m):] + tfckpt.VARIABLE_SUFFIX: np.asarray(v, np.float32) for k, v in sub.items()}
-        paths += tfckpt.write_bundle(path_prefix + name, tensors)
+        # Keras names the two instances of BaseEncoder 'base_encoder', 'base_encoder_1'
+        scope = "base_" + kind + ("" if i == 0 else f"_{i}")
+        paths += tfckpt.write_bundle(path_prefix + name, tensors, tfckpt.encode_object_graph(tensors, scope))
     return paths
 
 

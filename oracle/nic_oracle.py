@@ -313,11 +313,27 @@ def _ssim_per_channel(x, y, max_val=1.0, k1=0.01, k2=0.03, kernel=None):
     return (luminance * cs).mean(axis=(1, 2)), cs.mean(axis=(1, 2))
 
 
+def ms_ssim_scale_sizes(h: int, w: int) -> List[Tuple[int, int]]:
+    """Image size at each of the 5 scales: odd sizes are SYMMETRIC-padded by one, then 2x2
+    pooled, so every scale is ceil(previous / 2)."""
+    sizes = [(h, w)]
+    for _ in range(len(MSSSIM_WEIGHTS) - 1):
+        h, w = -(-h // 2), -(-w // 2)
+        sizes.append((h, w))
+    return sizes
+
+
+def ms_ssim_supported(h: int, w: int, filter_size: int = 11) -> bool:
+    """TF's _ssim_per_channel asserts every scale's H, W >= filter_size: 161 px and up."""
+    return all(min(s) >= filter_size for s in ms_ssim_scale_sizes(h, w))
+
+
 def ms_ssim_terms(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
     """Per-scale terms of ms_ssim: (N,C,5,2) float64 = (mean SSIM, mean cs) per channel and
     scale, before the relu and the weighted geometric mean."""
-    if min(img1.shape[1], img1.shape[2]) < 11 * 2 ** (len(MSSSIM_WEIGHTS) - 1):
-        raise ValueError(f"MS-SSIM needs images of at least 176x176, got {img1.shape[1:3]}")
+    if not ms_ssim_supported(img1.shape[1], img1.shape[2]):
+        raise ValueError(f"MS-SSIM needs every one of the 5 scales to hold the 11x11 window "
+                         f"(H, W >= 161), got {img1.shape[1:3]}")
     x = img1.astype(np.float64) * np.float32(1.0 / 255)
     y = img2.astype(np.float64) * np.float32(1.0 / 255)
     terms = []
@@ -336,7 +352,7 @@ def ms_ssim_terms(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
 def ms_ssim(img1: np.ndarray, img2: np.ndarray) -> np.ndarray:
     """tf.image.ssim_multiscale(img1, img2, max_val=255) for u8 (N,H,W,C) -> (N,).
 
-    Like TF, the coarsest of the 5 scales must still hold the 11x11 window: H, W >= 176."""
+    Like TF, every one of the 5 scales must still hold the 11x11 window: H, W >= 161."""
     t = ms_ssim_terms(img1, img2)
     # cs of scales 0..3 and SSIM of the last scale, each relu'd
     mcs = np.concatenate([t[:, :, :-1, 1], t[:, :, -1:, 0]], axis=-1)

@@ -7,6 +7,8 @@ Inputs come from the reference's own data files (read here as pixel data only):
   * imagenet_patches/00000..00003.jpg (128^2) -> case 'imagenet4'
   * kodim21.png crop [100:137, 200:253]      -> case 'odd37x53'   (TF-SAME odd sizes)
   * kodim21.png crop [0:256, 0:256] with Keras glorot/zero-bias weights -> 'kodim21_glorot'
+  * the whole kodim21.png (512 x 768)          -> case 'kodim21_full'  (BASELINE config 4, whole)
+  * its six 256^2 tiles (2 rows x 3 columns)  -> case 'kodim21_tiles' (config 4, tiled)
 The decoded pixels are stored, so the GPU box never decodes JPEG/PNG.
 
 Outputs (oracle, float64-accumulated convolutions): u8 latent, fp32 clipped pre-quant
@@ -47,14 +49,62 @@ def load_inputs(ref_data: str):
     }
 
 
+SAMPLE_STRIDE = 37  # full-resolution cases keep every 37th pre-quant value (size budget)
+
+
+def near_half(f: np.ndarray) -> np.ndarray:
+    """Codes whose oracle x*255 lies within 1e-3 of a .5 rounding boundary (may flip +-1)."""
+    v = f.astype(np.float64) * 255
+    return np.abs(v - np.floor(v) - 0.5) < 1e-3
+
+
+def full_resolution_cases(ref_data: str, w, manifest):
+    """SURVEY §8c golden vectors (3): the whole kodim21 (512 x 768, run as one image like
+    utils.py:46-62) and its six non-overlapping 256^2 tiles (config 4's tiled form).  The
+    pre-quant latent is kept only at every SAMPLE_STRIDE-th value plus a packed bitmask of
+    the near-.5 codes; latents and reconstructions are stored whole."""
+    from PIL import Image
+
+    kod = np.array(Image.open(os.path.join(ref_data, "kodak_img", "kodim21.png")).convert("RGB"))
+    assert kod.shape == (512, 768, 3), kod.shape
+    x = np.ascontiguousarray(kod[None])
+    tiles = np.stack([kod[256 * ty:256 * ty + 256, 256 * tx:256 * tx + 256] for ty in range(2) for tx in range(3)])
+    for name, xi in (("kodim21_full", x), ("kodim21_tiles", tiles)):
+        f = O.encode_f32(w, xi)
+        z = O.quantise_u8(f)
+        r = O.quantise_u8(O.decode_f32(w, z))
+        near = near_half(f)
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), latent=z, recon=r,
+                            prequant_sample=f.ravel()[::SAMPLE_STRIDE], near_half=np.packbits(near.ravel()),
+                            counts=O.histograms(z).astype(np.int32), bits=O.hist_entropy(z),
+                            **({"x": x} if name == "kodim21_full" else {}))
+        manifest["cases"][name] = {
+            "init": "spread", "x_shape": list(xi.shape), "latent_shape": list(z.shape),
+            "recon_shape": list(r.shape), "psnr_db": O.psnr(xi, r), "zero_codes": float(np.mean(z == 0)),
+            "codes_near_half": int(near.sum()), "sample_stride": SAMPLE_STRIDE,
+            "ms_ssim": [float(v) for v in O.ms_ssim(xi, r)],
+        }
+        print(name, manifest["cases"][name])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-data", default="/root/reference/data")
+    ap.add_argument("--only-full", action="store_true", help="regenerate only the full-resolution kodim21 cases")
     args = ap.parse_args()
     manifest = {"seed": 0, "oracle_acc": "float64", "weights": {}, "cases": {}}
+    if args.only_full:
+        with open(os.path.join(OUT, "manifest.json")) as fh:
+            manifest = json.load(fh)
     wsets = {init: W.seeded_weights(0, init=init) for init in ("spread", "glorot")}
     for init, w in wsets.items():
+        assert manifest["weights"].get(init, W.digest(w)) == W.digest(w), "weight generator drifted"
         manifest["weights"][init] = W.digest(w)
+    full_resolution_cases(args.ref_data, wsets["spread"], manifest)
+    if args.only_full:
+        with open(os.path.join(OUT, "manifest.json"), "w") as fh:
+            json.dump(manifest, fh, indent=1, sort_keys=True)
+        return
     for name, (x, init) in load_inputs(args.ref_data).items():
         w = wsets[init]
         x = np.ascontiguousarray(x, dtype=np.uint8)
@@ -67,8 +117,7 @@ def main():
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), x=x, latent=z, prequant=f, recon=r,
                             counts=counts.astype(np.int32), bits=bits)
         # distance of x*255 to the nearest .5 rounding boundary (codes that may flip)
-        v = f.astype(np.float64) * 255
-        near = int(np.sum(np.abs(v - np.floor(v) - 0.5) < 1e-3))
+        near = int(near_half(f).sum())
         manifest["cases"][name] = {
             "init": init, "x_shape": list(x.shape), "latent_shape": list(z.shape), "recon_shape": list(r.shape),
             "psnr_db": O.psnr(x, r[:, :x.shape[1], :x.shape[2]]),

@@ -1,0 +1,64 @@
+"""Child process of tests/test_gpu_parallel.py: config 3's sharded pass through RCCL.
+
+One rank (world size 1 -- the GPU box has one GPU; the 8-GPU node is the driver's) inits
+the "nccl" (= RCCL) process group on cuda:0, broadcasts the weights from rank 0, runs
+``parallel.run_sharded`` with the real HIP ``Codec`` and gathers latents, recons and
+entropy rows to rank 0 -- every collective of the config-3 path on the device -- then
+checks them against the CPU oracle.  Prints NCCL-OK on success.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    from neural_network_image_compression_amd import weights as W
+    from neural_network_image_compression_amd.codec import Codec
+    from neural_network_image_compression_amd.parallel import broadcast_weights, run_sharded, shard_range
+    from oracle import nic_oracle as O
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        assert dist.get_backend() == "nccl"
+        w = broadcast_weights(W.seeded_weights(0), dist)
+        assert W.digest(w) == W.digest(W.seeded_weights(0))
+        n_total = 3
+        x = np.random.default_rng(33).integers(0, 256, (n_total, 48, 64, 3), dtype=np.uint8)
+        lo, hi = shard_range(n_total, 1, 0)
+        codec = Codec(0)
+        codec.set_weights(w)
+        z, r, b = run_sharded(codec, torch.from_numpy(x[lo:hi]).cuda(), n_total, dist, dst=0)
+        torch.cuda.synchronize()
+        z, r, b = z.cpu().numpy(), r.cpu().numpy(), b.cpu().numpy()
+        f_ref = O.encode_f32(w, x)
+        d = z.astype(int) - O.quantise_u8(f_ref).astype(int)
+        v = f_ref.astype(np.float64) * 255
+        near = np.abs(v - np.floor(v) - 0.5) < 1e-3
+        assert np.abs(d).max() <= 1 and not np.any((d != 0) & ~near), "latent parity"
+        r_ref = O.decode(w, z)
+        assert np.abs(r.astype(int) - r_ref.astype(int)).max() <= 1 and O.psnr(r, r_ref) >= 50.0, "recon parity"
+        np.testing.assert_allclose(b, O.hist_entropy(z).reshape(3, n_total).T, rtol=0, atol=2e-6)
+        # a plain gather of rows to all ranks (dst=None: all_gather) on the device too
+        from neural_network_image_compression_amd.parallel import gather_rows
+        g = gather_rows(torch.from_numpy(z).cuda(), n_total, dist, dst=None)
+        assert torch.equal(g.cpu(), torch.from_numpy(z))
+    finally:
+        dist.destroy_process_group()
+    print("NCCL-OK")
+
+
+if __name__ == "__main__":
+    main()

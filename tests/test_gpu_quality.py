@@ -40,7 +40,10 @@ def _pairs():
     smooth = np.clip(smooth - smooth.min() + 40, 0, 255).astype(np.uint8)
     smooth2 = np.clip(smooth.astype(int) + rng.integers(-6, 7, smooth.shape), 0, 255).astype(np.uint8)
     indep = rng.integers(0, 256, (1, 180, 176, 3), dtype=np.uint8)
+    small = rng.integers(0, 256, (2, 161, 161, 3), dtype=np.uint8)  # smallest size TF accepts
     return {
+        "smallest_161x161": (small, np.clip(small.astype(int) + rng.integers(-30, 31, small.shape), 0, 255
+                                            ).astype(np.uint8)),
         "noise_vs_noisy": (x, noisy),
         "odd_177x203": (smooth, smooth2),
         "independent_noise": (indep, rng.integers(0, 256, indep.shape, dtype=np.uint8)),
@@ -48,7 +51,8 @@ def _pairs():
     }
 
 
-@pytest.mark.parametrize("case", ["noise_vs_noisy", "odd_177x203", "independent_noise", "identical"])
+@pytest.mark.parametrize("case", ["noise_vs_noisy", "odd_177x203", "independent_noise", "identical",
+                                  "smallest_161x161"])
 def test_ms_ssim_vs_oracle(case, codec):
     a, b = _pairs()[case]
     got, terms = codec.ms_ssim(_dev(a), _dev(b), per_scale=True)
@@ -72,7 +76,7 @@ def test_ms_ssim_codec_recon(codec, golden):
 
 
 def test_ms_ssim_errors(codec):
-    a = _dev(np.zeros((1, 175, 200, 3), np.uint8))
+    a = _dev(np.zeros((1, 160, 200, 3), np.uint8))  # scale 4 would be 10 px: below the 11-px window
     with pytest.raises(ValueError):
         codec.ms_ssim(a, a)
     b = _dev(np.zeros((1, 200, 200, 3), np.uint8))

@@ -170,7 +170,25 @@ def test_ms_ssim_properties(golden):
     k = O._fspecial_gauss()
     assert k.shape == (11, 11) and k.sum() == pytest.approx(1.0) and k[5, 5] == k.max()
     with pytest.raises(ValueError):
-        O.ms_ssim(x[:, :128, :128], x[:, :128, :128])
+        O.ms_ssim(x[:, :160, :200], x[:, :160, :200])
+    # TF's rule is per scale (ceil halving, each >= 11 px): 161 -> 81 -> 41 -> 21 -> 11
+    assert O.ms_ssim_supported(161, 161) and not O.ms_ssim_supported(160, 300)
+    assert O.ms_ssim(x[:, :161, :161], x[:, :161, :161]) == pytest.approx([1.0], abs=1e-12)
+    from neural_network_image_compression_amd.quality import ms_ssim_supported
+    for h in range(150, 180):
+        assert ms_ssim_supported(h, 200) == O.ms_ssim_supported(h, 200) == (h >= 161)
+
+
+def test_power_of_two_weight_scaling_is_exact(golden, weights_spread):
+    """The range-guard test's weights (tests/test_gpu_parity.py range_scaled_weights): a layer
+    scaled by 2^17 and the next by 2^-17 leave every oracle output bit-identical (leaky is
+    positively homogeneous, power-of-two scaling is exact)."""
+    from tests.test_gpu_parity import range_scaled_weights
+    w = range_scaled_weights(weights_spread)
+    g = golden("kodim21_256")
+    f = O.encode_f32(w, g["x"])
+    np.testing.assert_array_equal(f, g["prequant"])
+    np.testing.assert_array_equal(O.decode(w, g["latent"]), g["recon"])
 
 
 def test_tile_patches_roundtrip():

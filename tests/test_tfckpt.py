@@ -89,3 +89,50 @@ def test_positional_layer_keys(tmp_path):
     back = W.load(str(tmp_path / "enc"), "encoder")
     for k, v in back.items():
         np.testing.assert_array_equal(v, w[k])
+
+
+def test_object_graph_written_and_decoded(tmp_path, weights_spread):
+    """save_tf writes _CHECKPOINTABLE_OBJECT_GRAPH (the TrackableObjectGraph object-based
+    restore walks): root -> layer attributes -> kernel / bias -> VARIABLE_VALUE with the
+    checkpoint key of every tensor in the bundle; the numeric reader still skips it."""
+    prefix = str(tmp_path / "ck" / "encoder")
+    paths = W.save_tf(weights_spread, prefix, "encoder")
+    assert len(paths) == 4
+    for name, scope in (("Y", "base_encoder"), ("CbCr", "base_encoder_1")):
+        nodes = tfckpt.read_object_graph(prefix + name)
+        keys = set(tfckpt.read_bundle(prefix + name))
+        assert tfckpt.OBJECT_GRAPH_KEY not in keys
+        root = nodes[0]
+        assert sorted(n for _, n in root["children"]) == ["conv1", "conv2", "conv3", "conv4", "conv8"]
+        seen = set()
+        for lid, lname in root["children"]:
+            layer = nodes[lid]
+            assert sorted(v for _, v in layer["children"]) == ["bias", "kernel"]
+            for vid, vname in layer["children"]:
+                (attr,) = nodes[vid]["attributes"]
+                assert attr == ("VARIABLE_VALUE", f"{scope}/{lname}/{vname}",
+                                f"{lname}/{vname}/.ATTRIBUTES/VARIABLE_VALUE")
+                seen.add(attr[2])
+        assert seen == keys
+    # the loader reads the bundle back unchanged
+    back = W.load(prefix, "encoder")
+    for k, v in back.items():
+        np.testing.assert_array_equal(v, weights_spread[k])
+    # a corrupted string tensor fails its checksum
+    dp = prefix + "Y.data-00000-of-00001"
+    raw = bytearray(open(dp, "rb").read())
+    raw[-3] ^= 0x10
+    open(dp, "wb").write(bytes(raw))
+    with pytest.raises(ValueError):
+        tfckpt.read_object_graph(prefix + "Y")
+
+
+def test_string_tensor_format():
+    """TF's WriteStringTensor layout: varint64 lengths, masked CRC32C of the lengths (as
+    uint32), then the bytes; the entry CRC extends over all three."""
+    blob, crc = tfckpt._string_tensor_bytes([b"abc"])
+    assert blob[0] == 3 and blob[5:] == b"abc"
+    assert blob[1:5] == tfckpt.struct.pack("<I", tfckpt.mask_crc(tfckpt.crc32c(tfckpt.struct.pack("<I", 3))))
+    c = tfckpt.crc32c(tfckpt.struct.pack("<I", 3))
+    c = tfckpt.crc32c(blob[1:5], c)
+    assert crc == tfckpt.crc32c(b"abc", c)

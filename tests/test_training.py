@@ -74,3 +74,24 @@ def test_trained_weights_into_hip_codec(tmp_path):
     x = _smooth(1, 64, 72, 4)
     z, f = enc.codec.encode(torch.from_numpy(x).cuda(), prequant=True)
     np.testing.assert_allclose(f.cpu().numpy(), O.encode_f32(tr.weights(), x), atol=2e-5)
+
+
+def test_adam_matches_keras_update():
+    """torch Adam with keras_adam_eps(step) reproduces tf.keras Adam's update rule
+    (lr_t = lr sqrt(1-b2^t)/(1-b1^t); theta -= lr_t m / (sqrt(v) + eps)), restated in float64."""
+    rng = np.random.default_rng(3)
+    theta0 = rng.standard_normal(64)
+    grads = [rng.standard_normal(64) * 10.0 ** rng.integers(-9, 1) for _ in range(6)]
+    lr, b1, b2, eps = 1e-4, 0.9, 0.999, 1e-7
+    th, m, v = theta0.copy(), np.zeros(64), np.zeros(64)
+    for t, g in enumerate(grads, 1):
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        th = th - lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t) * m / (np.sqrt(v) + eps)
+    p = torch.tensor(theta0, dtype=torch.float64, requires_grad=True)
+    opt = torch.optim.Adam([p], lr=lr, betas=(b1, b2), eps=eps)
+    for t, g in enumerate(grads, 1):
+        p.grad = torch.tensor(g)
+        opt.param_groups[0]["eps"] = T.keras_adam_eps(t)
+        opt.step()
+    np.testing.assert_allclose(p.detach().numpy(), th, rtol=0, atol=1e-15)
