@@ -28,6 +28,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <utility>
 
 #include "nic_kernels.h"
@@ -1038,6 +1039,61 @@ struct HaloPieces {
   }
 };
 
+// LDS-DMA halo pieces through a buffer resource (buffer_load_dwordx4 ... lds): the
+// resource spans one plane, so every halo slot above, below or outside the plane is out of
+// range and the DMA writes zeros (TF's SAME padding) with no per-piece address select.
+// Per lane and piece the 32-bit byte offset from the halo origin is precomputed once; a
+// tile adds its origin (one v_add per piece) and, only on the tiles whose halo crosses the
+// left or right image edge, retargets the slots of out-of-image columns out of range.
+constexpr unsigned kDmaOOR = 0x80000000u;  // an offset past any plane: the DMA writes zeros
+constexpr int kBufWord3 = 0x00020000;      // gfx9 raw-buffer resource word 3
+
+__device__ __forceinline__ void dma16_buf(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)lds_wave_base, 16, (int)voff, 0, 0, 0);
+}
+
+template <class G, int CIN, int NPW>
+struct HaloDma {
+  static_assert(G::HW <= 15, "halo column packed into the low 4 bits of a 16-B aligned offset");
+  static constexpr int PSS = G::PSB / 16, RPS = G::RPB / 16;
+  static constexpr int TOTAL = G::HH * RPS;
+  static constexpr int NPIECE = (TOTAL + 63) / 64;
+  static constexpr int NPP = (NPIECE + NPW - 1) / NPW;  // pieces per loader wave (upper bound)
+  // per lane and piece: byte offset of the slot from the halo origin pixel (16-B aligned)
+  // | its halo column in bits 0..3; kDmaOOR for pad slots
+  unsigned off[NPP];
+  __device__ __forceinline__ void init(int pw, int lane, int W) {
+#pragma unroll
+    for (int i = 0; i < NPP; ++i) {
+      const int q = (pw + i * NPW) * 64 + lane;
+      const int row = q / RPS, r = q - row * RPS;
+      const int sp = r / PSS, k = r - sp * PSS;
+      const int x = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
+      // data slots (the rest is pad); swizzled records (G::SWZ) hold chunk k ^ swz(x) in slot k
+      const bool read = q < TOTAL && sp < G::HW && (G::SWZ || k < CIN / 4);
+      const int slot = G::SWZ ? G::chunk_at(k, x) : k;
+      off[i] = read ? (unsigned)((row * W + x) * CIN * 4 + slot * 16) | (unsigned)x : kDmaOOR;
+    }
+  }
+  // DMA the halo with origin (gy0, gx0) of the plane at `plane` (plane_bytes long) into buf
+  __device__ __forceinline__ void issue(char* buf, const char* plane, unsigned plane_bytes, int W, int gy0, int gx0,
+                                        int pw) const {
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)plane, (short)0, (int)plane_bytes,
+                                                                          kBufWord3);
+    const unsigned org = (unsigned)((gy0 * W + gx0) * CIN * 4);  // may wrap: then out of range
+    const bool edge = gx0 < 0 || gx0 + G::HW > W;                // wave-uniform
+#pragma unroll
+    for (int i = 0; i < NPP; ++i) {
+      const int piece = pw + i * NPW;
+      if (NPP * NPW > NPIECE && piece >= NPIECE) break;  // wave-uniform
+      const unsigned o = off[i];
+      unsigned v = (o & ~15u) + org;
+      if (edge && ((unsigned)(gx0 + (int)(o & 15u)) >= (unsigned)W || o == kDmaOOR)) v = kDmaOOR;
+      dma16_buf(rsrc, v, buf + piece * 1024);
+    }
+  }
+};
+
 // ------------------------------------------------------------------------------------
 // Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16) over a
 // stride-1 window of KH x KW taps: the k3 s1 layers (KH = KW = 3), and each of the four
@@ -1119,7 +1175,13 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   static_assert(!(TRP && RESID), "no residual on the transposed phases");
   static_assert(!PROJ || (TRP && COUT == 64 && TH * TW == 64), "projection: dconv7 8x8 tiles");
   using G = GeomWS<CIN, TH, TW>;
-  using HP = HaloPieces<G, CIN, CIN, NW>;
+  // halo DMA: buffer-resource pieces (HaloDma) for the plain and projection variants; the
+  // residual variant keeps the global_load_lds pieces (HaloPieces), measured 6 % faster there
+  // (same-box A/B: with HaloDma its stream carries ~8x the s_waitcnt instructions -- exact
+  // lgkmcnt counts instead of lgkmcnt(0) drains -- which the residual epilogue's partner
+  // wave cannot absorb), while HaloDma saves 2-3 % on conv3 / dconv5 / dconv7
+  constexpr bool kBufHalo = !RESID;
+  using HP = std::conditional_t<kBufHalo, HaloDma<G, CIN, NW>, HaloPieces<G, CIN, CIN, NW>>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1170,7 +1232,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   }
 
   HP hp;
-  hp.init(wave, lane);
+  const unsigned plane_bytes = (unsigned)((size_t)a.H * a.W * CIN * 4);
+  if constexpr (kBufHalo)
+    hp.init(wave, lane, a.W);
+  else
+    hp.init(wave, lane);
   auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
     const int t = bi + i * nb;
     const int pl = t / per_plane;
@@ -1182,8 +1248,12 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   auto issue = [&](int i) {
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
-    hp.template issue<true>(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4,
-                            a.zero16, a.H, a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
+    if constexpr (kBufHalo)
+      hp.issue(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * plane_bytes, plane_bytes, a.W,
+               t0y - a.pad_y, t0x - a.pad_x, wave);
+    else
+      hp.template issue<true>(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * plane_bytes, a.zero16,
+                              a.H, a.W, t0y - a.pad_y, t0x - a.pad_x, 0, wave);
   };
 
   f32x4 acc[MT];
@@ -1215,6 +1285,9 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
+#ifdef NIC_DIAG_NOEPI  // diagnostic build only: no epilogue arithmetic (wrong results)
+        u32x4 q = __builtin_bit_cast(u32x4, acc[m]);
+#else
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
@@ -1228,6 +1301,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         f16x4 hi, lo;
         split4(v, hi, lo);
         u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
+#endif
         if constexpr (PROJ) {  // chunk (g & 1) * 8 + 2w + g / 2 of pixel 16m + l16
           const int pp = 16 * m + l16, ch = (g & 1) * 8 + 2 * wave + (g >> 1);
           *(u32x4*)(hproj + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
@@ -1238,6 +1312,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
       }
     }
     f16x8 ah[KST], al[KST];
+    // PROJ: the next halo's DMA issue runs before the projection barrier, where it overlaps
+    // the other waves finishing their epilogues (buffer (i+1)&1 was last read by tile i-1's
+    // stream, which every wave finished before the top barrier)
+    if constexpr (PROJ)
+      if (i + 1 < ntile) issue(i + 1);
     if constexpr (PROJ)
       if (i > 0) {
         lds_reads_done();  // lgkmcnt(0): this wave's hproj writes have landed
@@ -1249,7 +1328,8 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
           al[ks] = *(const f16x8*)(hproj + pp * 256 + (((8 + 4 * ks + g) ^ (pp & 15)) << 4));
         }
       }
-    if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
+    if constexpr (!PROJ)
+      if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
     if constexpr (PROJ)
       if (i > 0) {
         float* dst = a.proj +
@@ -1320,10 +1400,12 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
+#ifndef NIC_DIAG_NOLDS  // diagnostic build: the fragments of step 0 reused (wrong results)
         if (st + 1 < NSTEP) {
           fb[m][0] = frag(m, st + 1, 0);
           fb[m][1] = frag(m, st + 1, 1);
         }
+#endif
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
       }
     }
@@ -2687,6 +2769,8 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   const long long nt = per_plane * a.P;
   if (nt == 0) return hipSuccess;
   if (nt > INT32_MAX || a.P != 3 * a.nimg) return hipErrorInvalidValue;
+  // HaloDma: 32-bit plane offsets, out-of-range slots past the plane (kDmaOOR)
+  if ((long long)a.H * a.W * CIN * 4 >= (1LL << 30)) return hipErrorInvalidValue;
   a.ntiles = (int)nt;
   const int nset = TRP ? 4 : 1;
   const int taps[4] = {TRP ? 4 : 9, 6, 6, 9};
