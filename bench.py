@@ -300,7 +300,7 @@ def main():
             dec(enc(xh))
         hp = (time.perf_counter() - t0) / reps
         host_path = {"mp_per_s": round(B * H * W / 1e6 / hp, 1), "ms_per_batch": round(hp * 1e3, 3),
-                     "path": "Encoder()(numpy) -> Decoder()(numpy): pageable host arrays, PCIe both ways"}
+                     "path": "Encoder()(numpy) -> Decoder()(numpy): host arrays through pinned staging, 4 chunks with H2D / device pass / D2H overlapped on two streams"}
     quality = None
     if args.workload in ("config2", "kodak") and min(H, W) >= 161:
         # device MS-SSIM (nic_ms_ssim) and PSNR (nic_sq_err) of the batch's reconstruction;

@@ -256,8 +256,82 @@ class Codec:
         return out
 
 
+class _HostPipe:
+    """Host-array surface of a device call: pinned staging buffers (grown on demand, reused)
+    and the batch cut into chunks so that chunk k's host->pinned copy and H2D DMA (copy
+    stream), chunk k-1's device pass (compute stream) and chunk k-2's D2H DMA overlap.
+    The reference's surface moves NumPy in and out around every call (encoder.py:38-47,
+    decoder.py:39-48); this is that hand-off, pipelined.  Every call synchronises before it
+    returns (NumPy out), so the staging buffers are free again for the next call."""
+
+    def __init__(self, device: int):
+        torch = _torch()
+        self.device = device
+        self.copy = torch.cuda.Stream(device)
+        self.comp = torch.cuda.Stream(device)
+        self._pin = {}
+
+    def _pinned(self, key: str, nbytes: int):
+        torch = _torch()
+        buf = self._pin.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+            self._pin[key] = buf
+        return buf
+
+    def run(self, a: np.ndarray, fn, out_tail, chunks: int) -> np.ndarray:
+        """fn: device u8 (n, *a.shape[1:]) -> device u8 (n, *out_tail); returns NumPy."""
+        torch = _torch()
+        n = a.shape[0]
+        out = np.empty((n,) + tuple(out_tail), np.uint8)
+        if n == 0:
+            return out
+        a = np.ascontiguousarray(a)
+        in_row, out_row = a[0].nbytes, out[0].nbytes
+        pin_in = self._pinned("in", n * in_row)
+        pin_out = self._pinned("out", n * out_row)
+        cur = torch.cuda.current_stream(self.device)
+        self.copy.wait_stream(cur)  # the caller's earlier work on this device comes first
+        self.comp.wait_stream(cur)
+        bounds = np.linspace(0, n, min(chunks, n) + 1).astype(int)
+        done = []
+        keep = []
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            if hi == lo:
+                continue
+            src = pin_in[lo * in_row:hi * in_row]
+            src.numpy()[:] = a[lo:hi].reshape(-1)  # host copy into pinned memory
+            with torch.cuda.stream(self.copy):
+                x = torch.empty((hi - lo,) + a.shape[1:], dtype=torch.uint8, device=f"cuda:{self.device}")
+                x.view(-1).copy_(src, non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(self.copy)
+            with torch.cuda.stream(self.comp):
+                self.comp.wait_event(ev_in)
+                y = fn(x)
+                ev_y = torch.cuda.Event()
+                ev_y.record(self.comp)
+            with torch.cuda.stream(self.copy):
+                self.copy.wait_event(ev_y)
+                pin_out[lo * out_row:hi * out_row].copy_(y.reshape(-1), non_blocking=True)
+                ev_out = torch.cuda.Event()
+                ev_out.record(self.copy)
+            keep.append((x, y))  # device buffers stay alive until their DMA is done
+            done.append((lo, hi, ev_out))
+        flat = out.reshape(-1)
+        po = pin_out.numpy()
+        for lo, hi, ev in done:  # chunk k's pinned -> NumPy copy overlaps chunk k+1's work
+            ev.synchronize()
+            flat[lo * out_row:hi * out_row] = po[lo * out_row:hi * out_row]
+        cur.wait_stream(self.copy)
+        return out
+
+
 class ProClass:
     """utils.py:15-62: shared Y/CbCr model holder (kind 'encoder' or 'decoder')."""
+
+    #: chunks of the host-array pipeline (``_HostPipe``) per call
+    host_chunks = 4
 
     kind = ""
 
@@ -283,9 +357,16 @@ class ProClass:
         a = _as_u8_array(x.cpu().numpy() if isinstance(x, torch.Tensor) else x, type(self).__name__)
         if a.ndim != 4:
             raise ValueError(f"{type(self).__name__}: expected a 4-D NHWC batch, got shape {a.shape}")
-        dev = torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{self.codec.device}")
-        out = self._device_call(dev)
-        return out.cpu().numpy()
+        self._check_host(a)
+        if getattr(self, "_pipe", None) is None:
+            self._pipe = _HostPipe(self.codec.device)
+        return self._pipe.run(a, self._device_call, self._out_tail(a.shape), self.host_chunks)
+
+    def _check_host(self, a: np.ndarray) -> None:
+        pass
+
+    def _out_tail(self, shape):
+        raise NotImplementedError
 
 
 class Encoder(ProClass):
@@ -295,6 +376,14 @@ class Encoder(ProClass):
 
     def _device_call(self, x):
         return self.codec.encode(x)
+
+    def _check_host(self, a):
+        if a.shape[3] != 3:
+            raise ValueError(f"Encoder: expected shape (N,H,W,3), got {a.shape}")
+
+    def _out_tail(self, shape):
+        h8, w8 = _lib.latent_shape(shape[1], shape[2])
+        return (h8, w8, 96)
 
     def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
         """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``.
@@ -312,6 +401,13 @@ class Decoder(ProClass):
 
     def _device_call(self, z):
         return self.codec.decode(z)
+
+    def _check_host(self, a):
+        if a.shape[3] != 96:
+            raise ValueError(f"Decoder: expected shape (N,h,w,96), got {a.shape}")
+
+    def _out_tail(self, shape):
+        return (8 * shape[1], 8 * shape[2], 3)
 
     def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
         """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``."""

@@ -105,7 +105,10 @@ __device__ __forceinline__ uint8_t quant255(float v) {
 // at the end: a value at or beyond the f16 limit would split into +-inf.  NaN needs an inf
 // first (finite operands; products bounded by the weight pre-scale), so the max catches it.
 __device__ __forceinline__ void range_track(float& m, const f32x4& v) {
-  m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  // two v_max3_f32 with |.| source modifiers (fmaxf's NaN canonicalisation would add a
+  // v_max per value); NaN sources are not needed here (see above)
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[0]), "v"(v[1]));
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[2]), "v"(v[3]));
 }
 __device__ __forceinline__ void range_report(const RangeGuard& rg, float m) {
   if (!(m < kF16Limit) && rg.flag) atomicExch(rg.flag, rg.epoch);  // vector atomic, rare
@@ -495,13 +498,39 @@ struct GeomX3 {
   }
 };
 
+#ifndef NIC_MIX_SPLIT
+#define NIC_MIX_SPLIT 1
+#endif
 __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
+#if NIC_MIX_SPLIT
+  // per pair: hi = cvt_pk_f16 (RNE); the exact differences v - f32(hi) by v_fma_mix_f32 with
+  // hi read as an f16 half (one op each instead of cvt back + subtract); lo = cvt_pk_f16 of
+  // them.  v - f32(hi) is exact in fp32 (Sterbenz; hi within 2x of v or both tiny), so this
+  // is bit-identical to (_Float16)(v - (float)(_Float16)v) (checked over 16M values,
+  // tools/mixcheck.hip).
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 H, L;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    unsigned h, l;
+    float d0, d1;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(v[2 * k]), "v"(v[2 * k + 1]));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(h), "v"(v[2 * k]));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(h), "v"(v[2 * k + 1]));
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(d0), "v"(d1));
+    H[k] = h;
+    L[k] = l;
+  }
+  hi = __builtin_bit_cast(f16x4, H);
+  lo = __builtin_bit_cast(f16x4, L);
+#else
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const _Float16 h = (_Float16)v[r];
     hi[r] = h;
     lo[r] = (_Float16)(v[r] - (float)h);  // exact difference, then RNE to f16
   }
+#endif
 }
 
 // Stage the input halo of one block into LDS as f16 hi / lo images.  Loads are issued in
@@ -1320,7 +1349,9 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     if constexpr (PROJ)
       if (i > 0) {
         lds_reads_done();  // lgkmcnt(0): this wave's hproj writes have landed
+#ifndef NIC_DIAG_NOBAR2  // diagnostic build: no projection barrier (racy, wrong results)
         stage_barrier();   // the whole tile's channels are in hproj
+#endif
         const int pp = 16 * wave + l16;
 #pragma unroll
         for (int ks = 0; ks < KST; ++ks) {
@@ -1335,8 +1366,12 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         float* dst = a.proj +
                      ((((size_t)ep_p * 4 + 2 * py + px) * a.tiles_y + ep_y / TH) * a.tiles_x + ep_x / TW) * (25 * 64) +
                      16 * wave + 4 * g;
+#ifndef NIC_DIAG_NOPROJ  // diagnostic build: no projection MFMAs / stores (wrong results)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
+#else
+        for (int nt = 0; nt < 0; ++nt) {
+#endif
           f16x8 wh[KST], wl[KST];
 #pragma unroll
           for (int ks = 0; ks < KST; ++ks) {
@@ -1790,6 +1825,296 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   }
 #endif
 #undef WS2_MARK
+}
+
+// conv1 + conv2 fused and software-pipelined (split-f16; encoder.py:10-11, 20-21 with the
+// colour front end utils.py:74-77), the tap-split weight-stationary form of ws2_wave with
+// two conv2 halo buffers so that conv1 of tile i+1 runs beside conv2 of tile i:
+//   [B_top] ts 0: epilogue of tile i-1 (own sums + the ts 1 partials) | ts 1: colour patch
+//   of tile i+1 from RGB bytes loaded one tile earlier
+//   [B1] ts 0: conv1 share of tile i+1 -> conv2 stream of tile i | ts 1: RGB loads of tile
+//   i+2, conv2 stream of tile i, its partial sums, conv1 share of tile i+1.
+// Two barriers per tile (the unpipelined form needs three, and its conv1 phase ran on all
+// 8 waves at once with the matrix pipes idle); SIMD partners (w, w + 4) are the two tap
+// halves of one channel group and meet the conv1 VALU work of one with the conv2 MFMA
+// stream of the other.  conv1 of tile k writes halo buffer k & 1; the patch and the partial
+// tile are single buffers (each barrier orders their reuse).  LDS: 2 x 57 KB + 16 + 9.5 KB.
+template <int TS>
+__device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
+  constexpr int CIN = 32, COUT = 64, NTS = 2, TH = 8, TW = 8, MT = 4, NCG = 4, KST = 1, NW = 8;
+  constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
+  using G = GeomS2<CIN, TH, TW>;
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+  constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
+  char* part = lds + 2 * G::HALO_BYTES;         // [NCG] partial tiles of the ts = 1 waves
+  float* plane = (float*)(part + NCG * PART);   // colour-plane patch
+  float* lut = plane + C12_PH * C12_PP;         // u8 -> fp32 / 255
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave % NCG;
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int per_plane = a.tiles_y * a.tiles_x;
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  const int ntot = np * per_plane;
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+
+  f16x8 wr[NT][KST][2];
+  {
+    const char* wsrc = (const char*)a.wx + ((size_t)model * 25 + T0) * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          wr[t][ks][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
+                                          ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
+  }
+  const float scale = a.wscale[model];
+  const int co0 = cg * 16 + 4 * g;
+  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
+  int boff[MT];  // B fragment of pixel tile m at tap (0, 0): halo row 2 (2m + l16/8), column l16 % 8
+#pragma unroll
+  for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
+  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
+    const int t = bi + i * nb;
+    const int pl = t / per_plane;
+    p = p0 + pl;
+    const int r = t - pl * per_plane, ty = r / a.tiles_x;
+    t0y = ty * TH;
+    t0x = (r - ty * a.tiles_x) * TW;
+  };
+
+  // conv1 A fragments / bias / scale and this lane's im2col tap offsets (-1: pad tap >= 25)
+  f16x8 A1[2][2];
+  f32x4 b1[2];
+  {
+    const f16x8* wa = (const f16x8*)a.wx1 + (size_t)model * 2 * 2 * 64 + lane;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) A1[ct][hl] = wa[(ct * 2 + hl) * 64];
+      b1[ct] = *(const f32x4*)(a.bias1 + model * 32 + 16 * ct + 4 * g);
+    }
+  }
+  const float scale1 = a.wscale1[model];
+  int toff[4];  // patch offsets of this lane's 4 tap pairs (k = 2 * pair + e: pair = kh * 3 + kw / 2)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pr = 4 * g + j;
+    toff[j] = pr < 15 ? (pr / 3) * C12_PP + 2 * (pr % 3) : -1;
+  }
+  constexpr int NRGB = (C12_PH * C12_PH + 255) / 256;  // patch pixels per ts = 1 thread
+  uint32_t rgb_b[NRGB][2];  // raw bytes of this thread's patch pixels (ts = 1 waves): r | g << 8, b
+  uint32_t rgb_in = 0;      // bit j: pixel j lies inside the image
+  int pl_type = 0;          // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
+  const int tid1 = (int)threadIdx.x - 256;
+  auto rgb_load = [&](int i) {  // plain loads, unpacked by the next phase A (no wait before the MFMAs)
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    const int n = p % a.nimg;
+    pl_type = p / a.nimg;
+    const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
+    const uint8_t* img = a.rgb + (size_t)n * a.H0 * a.W0 * 3;
+    rgb_in = 0;
+#pragma unroll
+    for (int j = 0; j < NRGB; ++j) {
+      const int idx = tid1 + 256 * j;
+      const int r = idx / C12_PH, c = idx - r * C12_PH;
+      const int gy = py0 + r, gx = px0 + c;
+      const bool inside = idx < C12_PH * C12_PH && (unsigned)gy < (unsigned)a.H0 && (unsigned)gx < (unsigned)a.W0;
+      const int cy = min(max(gy, 0), a.H0 - 1), cx = min(max(gx, 0), a.W0 - 1);
+      const uint8_t* px = img + ((size_t)cy * a.W0 + cx) * 3;
+      rgb_b[j][0] = *(const uint16_t*)px;  // r, g (unaligned 2-B load)
+      rgb_b[j][1] = px[2];
+      rgb_in |= (inside ? 1u : 0u) << j;
+    }
+  };
+  // colour plane of the patch (utils.py:74-77: x/255, ((r k0 + g k1) + b k2) + off, every op
+  // rounded), zero outside the image (conv1's SAME padding)
+  auto patch = [&]() {
+    const float* kk = c_ycbcr + pl_type * 3;
+    const float off = c_ycbcr_off[pl_type];
+#pragma unroll
+    for (int j = 0; j < NRGB; ++j) {
+      const int idx = tid1 + 256 * j;
+      if (idx < C12_PH * C12_PH) {
+        const int r = idx / C12_PH, c = idx - r * C12_PH;
+        plane[r * C12_PP + c] = ((rgb_in >> j) & 1)
+                                    ? __fadd_rn(project(kk, lut[rgb_b[j][0] & 255], lut[rgb_b[j][0] >> 8], lut[rgb_b[j][1]]), off)
+                                    : 0.f;
+      }
+    }
+  };
+  float rmax = 0.f;  // range guard of the split outputs (conv2's, and conv1's into the halo)
+  // conv1 of tile i on the 19 x 19 halo pixels into halo buffer i & 1: px-tiles of 16, two
+  // 16-channel tiles each, three px-tiles per wave software-pipelined
+  auto conv1 = [&](int i) {
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    char* halo = lds + (i & 1) * G::HALO_BYTES;
+    const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;  // halo origin, conv1-output coords
+    constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + NW - 1) / NW;
+    f32x2 xv[PTW][4];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+      const int q = 16 * (wave + NW * u) + l16;
+      const int qq = q < G::HH * G::HW ? q : 0;
+      const int hy = qq / G::HW, hx = qq - hy * G::HW;
+      const float* pb = plane + 2 * hy * C12_PP + 2 * hx;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[u][j] = toff[j] >= 0 ? *(const f32x2*)(pb + toff[j]) : (f32x2){0.f, 0.f};
+    }
+    f16x8 bh[PTW], bl[PTW];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = xv[u][j >> 1][j & 1];
+        const _Float16 hh = (_Float16)x;
+        bh[u][j] = hh;
+        bl[u][j] = (_Float16)(x - (float)hh);
+      }
+    f32x4 c1[PTW][2];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl[u], c1[u][ct], 0, 0, 0);
+        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh[u], c1[u][ct], 0, 0, 0);
+      }
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+      const int pt = wave + NW * u;
+      if (pt >= NPT) break;  // wave-uniform
+      const int q = 16 * pt + l16;
+      const bool qv = q < G::HH * G::HW;
+      const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
+      const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
+        range_track(rmax, v);
+        f16x4 hi, lo;
+        split4(v, hi, lo);
+        if (qv) {
+          char* d = halo + hy * G::RPB + G::col(hx) * G::PSB + (16 * ct + 4 * g) * 2;
+          *(f16x4*)d = hi;
+          *(f16x4*)(d + CIN * 2) = lo;
+        }
+      }
+    }
+  };
+  f32x4 acc[MT];
+  // conv2 of tile i: this wave's NT taps x MT pixel tiles on halo buffer i & 1, B fragments
+  // DEPTH groups ahead
+  auto stream = [&](int i) {
+    const char* buf = lds + (i & 1) * G::HALO_BYTES;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    constexpr int NG = NT * KST * MT, DEPTH = 3;
+    auto grp_off = [&](int gq) {
+      const int st = gq / MT, m = gq - st * MT;
+      const int t = T0 + st / KST, kh = t / 5, kw = t - kh * 5;
+      return boff[m] + kh * G::RPB + G::col(kw) * G::PSB;
+    };
+    f16x8 fb[DEPTH][2];
+#pragma unroll
+    for (int gq = 0; gq < DEPTH; ++gq) {
+      fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
+      fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    static_for<NG>([&](auto gqc) {
+      constexpr int gq = decltype(gqc)::value;
+      constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;
+      f16x8(&cur)[2] = fb[gq % DEPTH];
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], acc[m], 0, 0, 0);  // w_lo*a_hi
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], acc[m], 0, 0, 0);  // w_hi*a_lo
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], acc[m], 0, 0, 0);  // w_hi*a_hi
+      if constexpr (gq + DEPTH < NG) {
+        cur[0] = *(const f16x8*)(buf + grp_off(gq + DEPTH));
+        cur[1] = *(const f16x8*)(buf + grp_off(gq + DEPTH) + CIN * 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the stream order
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
+  auto epilogue = [&](int i) {  // ts 0: own sums + the ts 1 partials, bias, leaky, split, 16-B stores
+    int p, t0y, t0x;
+    tile_at(i, p, t0y, t0x);
+    const char* pp = part + cg * PART + lane * 16;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const f32x4 q = *(const f32x4*)(pp + m * 1024);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
+      const int oy = t0y + 2 * m + (l16 >> 3), ox = t0x + (l16 & 7);
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+      const bool inside = oy < a.OH && ox < a.OW;
+      if (inside) range_track(rmax, v);
+      f16x4 hi, lo;
+      split4(v, hi, lo);
+      const u32x4 qv = swap16_pair(hi, lo);
+      if (inside) *(u32x4*)(a.out_s + (((size_t)p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = qv;
+    }
+  };
+
+  // prologue: patch 0 -> conv1 0 (halo 0)
+  if constexpr (TS == 1)
+    if (ntile > 0) rgb_load(0);
+  for (int q = threadIdx.x; q < 256; q += 64 * NW) lut[q] = c_u8_to_unit[q];
+  for (int q = threadIdx.x; q < C12_PH * C12_PP; q += 64 * NW) plane[q] = 0.f;  // pad columns
+  __syncthreads();  // LUT and zeroed pads before any patch store
+  if constexpr (TS == 1) {
+    if (ntile > 0) patch();
+    if (ntile > 1) rgb_load(1);
+  }
+  lds_reads_done();
+  stage_barrier();  // patch 0 complete
+  if (ntile > 0) conv1(0);
+  for (int i = 0; i <= ntile; ++i) {
+    lds_reads_done();
+    stage_barrier();  // B_top: halo i complete, partials of tile i-1 written, the patch free
+    if constexpr (TS == 0) {
+      if (i > 0) epilogue(i - 1);
+    } else {
+      if (i + 1 < ntile) patch();  // tile i+1, from the RGB bytes loaded during tile i-1's phase B
+    }
+    if (i == ntile) break;
+    lds_reads_done();
+    stage_barrier();  // B1: patch of tile i+1 complete; the partial tiles read
+    if constexpr (TS == 0) {
+      if (i + 1 < ntile) conv1(i + 1);
+      stream(i);
+    } else {
+      if (i + 2 < ntile) rgb_load(i + 2);  // in flight during the stream
+      stream(i);
+      char* pp = part + cg * PART + lane * 16;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+      if (i + 1 < ntile) conv1(i + 1);
+    }
+  }
+  range_report(a.rg, rmax);
+}
+
+__global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
+  using G = GeomS2<32, 8, 8>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + (C12_PH * C12_PP + 256) * 4];
+  int gi = 0;
+  while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
+  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < 4)
+    c12_wave<0>(a, lds, gi, bi, nb);
+  else
+    c12_wave<1>(a, lds, gi, bi, nb);
 }
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1>
@@ -2797,7 +3122,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
 
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
 // proportion to their planes.
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
 static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.tiles_y = (a.OH + TH - 1) / TH;
   a.tiles_x = (a.OW + 7) / 8;
@@ -2816,15 +3141,29 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = (int)by;
   a.ws_blk[2] = (int)(by + bc);
-  hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  if constexpr (PIPE12)
+    hipLaunchKernelGGL(conv12_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   return hipGetLastError();
 }
 
 bool conv12_fused() { return use_ws(); }
 
+// NIC_C12=serial selects the unpipelined fused kernel (conv_ws2_kernel FUSE1: one halo
+// buffer, conv1 between two barriers) for A/B runs
+static bool c12_serial() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_C12");
+    return e && e[0] == 's';
+  }();
+  return on;
+}
+
 hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st) {
   if (!a.rgb || !a.wx1 || !a.bias1 || a.H0 <= 0 || a.W0 <= 0) return hipErrorInvalidValue;
-  return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
+  if (c12_serial()) return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
+  return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
 }
 
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first match)
     (r"conv1_colour", "conv1"), (r"dconv8_colour", "dconv8"), (r"dconv8_x3", "dconv8"), (r"dconv8_strip", "dconv8"),
-    (r"conv_ws2_kernel<32, 64", "conv2"), (r"conv_ws2_kernel<64, 32", "conv8"),
+    (r"conv12_kernel", "conv2"), (r"conv_ws2_kernel<32, 64", "conv2"), (r"conv_ws2_kernel<64, 32", "conv8"),
     (r"<32, 64, 5, 2, false", "conv2"), (r"<64, 32, 5, 2, false", "conv8"),
     (r"<32, 64, 5, 2, true", "dconv1"), (r"<64, 64, 5, 2, true", "dconv7"),
     (r"dconv8_gather", "dconv8"), (r"conv_ws_kernel<64, 64, 8, 8, false, true", "dconv7"),
