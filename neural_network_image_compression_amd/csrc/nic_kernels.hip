@@ -1839,6 +1839,17 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 // halves of one channel group and meet the conv1 VALU work of one with the conv2 MFMA
 // stream of the other.  conv1 of tile k writes halo buffer k & 1; the patch and the partial
 // tile are single buffers (each barrier orders their reuse).  LDS: 2 x 57 KB + 16 + 9.5 KB.
+// u8 x -> fp32(x) / 255 correctly rounded without the LUT: q = x * fp32(1/255), then one
+// FMA residual correction (exact for all 256 bytes; same values as c_u8_to_unit)
+#ifndef NIC_C12_LUT
+#define NIC_C12_LUT 0
+#endif
+__device__ __forceinline__ float u8_unit(unsigned x) {
+  const float xf = (float)x, r = 0.0039215688593685627f;  // fp32(1/255)
+  const float q = __fmul_rn(xf, r);
+  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, xf), r, q);
+}
+
 template <int TS>
 __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int CIN = 32, COUT = 64, NTS = 2, TH = 8, TW = 8, MT = 4, NCG = 4, KST = 1, NW = 8;
@@ -1909,24 +1920,39 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   uint32_t rgb_in = 0;      // bit j: pixel j lies inside the image
   int pl_type = 0;          // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
   const int tid1 = (int)threadIdx.x - 256;
-  auto rgb_load = [&](int i) {  // plain loads, unpacked by the next phase A (no wait before the MFMAs)
+  // per thread and patch pixel j (idx = tid1 + 256 j): its byte offset from the patch origin
+  // in the image and its (row, column) packed r | c << 8 (0xffff: no pixel)
+  unsigned pix_off[NRGB], pix_rc[NRGB];
+  if constexpr (TS == 1) {
+#pragma unroll
+    for (int j = 0; j < NRGB; ++j) {
+      const int idx = tid1 + 256 * j;
+      const int r = idx / C12_PH, c = idx - r * C12_PH;
+      const bool ok = idx < C12_PH * C12_PH;
+      pix_off[j] = ok ? (unsigned)((r * a.W0 + c) * 3) : 0u;
+      pix_rc[j] = ok ? (unsigned)(r | c << 8) : 0xffffu;
+    }
+  }
+  // RGB bytes of tile i's patch: buffer loads over image n (rows above / below the image
+  // read zeros; the inside mask zeroes the rest), plain registers consumed by the next phase A
+  auto rgb_load = [&](int i) {
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
     const int n = p % a.nimg;
     pl_type = p / a.nimg;
     const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
-    const uint8_t* img = a.rgb + (size_t)n * a.H0 * a.W0 * 3;
+    const unsigned img_bytes = (unsigned)(a.H0 * a.W0 * 3);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.rgb + (size_t)n * img_bytes), (short)0, (int)img_bytes, kBufWord3);
+    const unsigned org = (unsigned)((py0 * a.W0 + px0) * 3);
     rgb_in = 0;
 #pragma unroll
     for (int j = 0; j < NRGB; ++j) {
-      const int idx = tid1 + 256 * j;
-      const int r = idx / C12_PH, c = idx - r * C12_PH;
-      const int gy = py0 + r, gx = px0 + c;
-      const bool inside = idx < C12_PH * C12_PH && (unsigned)gy < (unsigned)a.H0 && (unsigned)gx < (unsigned)a.W0;
-      const int cy = min(max(gy, 0), a.H0 - 1), cx = min(max(gx, 0), a.W0 - 1);
-      const uint8_t* px = img + ((size_t)cy * a.W0 + cx) * 3;
-      rgb_b[j][0] = *(const uint16_t*)px;  // r, g (unaligned 2-B load)
-      rgb_b[j][1] = px[2];
+      const int r = (int)(pix_rc[j] & 255), c = (int)(pix_rc[j] >> 8);
+      const bool inside = pix_rc[j] != 0xffffu && (unsigned)(py0 + r) < (unsigned)a.H0 && (unsigned)(px0 + c) < (unsigned)a.W0;
+      const unsigned v = inside ? pix_off[j] + org : kDmaOOR;
+      rgb_b[j][0] = __builtin_amdgcn_raw_buffer_load_b16(rs, (int)v, 0, 0);      // r, g
+      rgb_b[j][1] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(v + 2u), 0, 0);  // b
       rgb_in |= (inside ? 1u : 0u) << j;
     }
   };
@@ -1937,12 +1963,14 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     const float off = c_ycbcr_off[pl_type];
 #pragma unroll
     for (int j = 0; j < NRGB; ++j) {
-      const int idx = tid1 + 256 * j;
-      if (idx < C12_PH * C12_PH) {
-        const int r = idx / C12_PH, c = idx - r * C12_PH;
-        plane[r * C12_PP + c] = ((rgb_in >> j) & 1)
-                                    ? __fadd_rn(project(kk, lut[rgb_b[j][0] & 255], lut[rgb_b[j][0] >> 8], lut[rgb_b[j][1]]), off)
-                                    : 0.f;
+      if (pix_rc[j] != 0xffffu) {
+        const int r = (int)(pix_rc[j] & 255), c = (int)(pix_rc[j] >> 8);
+#if NIC_C12_LUT
+        const float r8 = lut[rgb_b[j][0] & 255], g8 = lut[rgb_b[j][0] >> 8], b8 = lut[rgb_b[j][1]];
+#else
+        const float r8 = u8_unit(rgb_b[j][0] & 255), g8 = u8_unit(rgb_b[j][0] >> 8), b8 = u8_unit(rgb_b[j][1]);
+#endif
+        plane[r * C12_PP + c] = ((rgb_in >> j) & 1) ? __fadd_rn(project(kk, r8, g8, b8), off) : 0.f;
       }
     }
   };
@@ -2000,11 +2028,12 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
         range_track(rmax, v);
         f16x4 hi, lo;
         split4(v, hi, lo);
-        if (qv) {
-          char* d = halo + hy * G::RPB + G::col(hx) * G::PSB + (16 * ct + 4 * g) * 2;
-          *(f16x4*)d = hi;
-          *(f16x4*)(d + CIN * 2) = lo;
-        }
+        // swap16_pair: even-g lanes hold the hi of channels 16 ct + 4 g .. +7, odd-g lanes
+        // the lo of the same 8: one 16-B store per lane (2-way bank conflicts with the
+        // 160-B records) instead of two 8-B stores (4-way)
+        const u32x4 q16 = swap16_pair(hi, lo);
+        if (qv)
+          *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * ct + 4 * (g & ~1)) * 2) = q16;
       }
     }
   };
@@ -2048,9 +2077,12 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
     const char* pp = part + cg * PART + lane * 16;
+    f32x4 q4[MT];  // all partial reads in flight before the first use
+#pragma unroll
+    for (int m = 0; m < MT; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const f32x4 q = *(const f32x4*)(pp + m * 1024);
+      const f32x4 q = q4[m];
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
       const int oy = t0y + 2 * m + (l16 >> 3), ox = t0x + (l16 & 7);
@@ -2079,29 +2111,61 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   lds_reads_done();
   stage_barrier();  // patch 0 complete
   if (ntile > 0) conv1(0);
+#ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
+  unsigned long long sx[8] = {}, sa, sb;
+  NIC_PNOW(sa);
+#define C12_MARK(kk)   \
+  do {                 \
+    NIC_PNOW(sb);      \
+    sx[kk] += sb - sa; \
+    sa = sb;           \
+  } while (0)
+#else
+#define C12_MARK(kk) \
+  do {               \
+  } while (0)
+#endif
   for (int i = 0; i <= ntile; ++i) {
+    C12_MARK(6);
     lds_reads_done();
     stage_barrier();  // B_top: halo i complete, partials of tile i-1 written, the patch free
+    C12_MARK(0);
     if constexpr (TS == 0) {
       if (i > 0) epilogue(i - 1);
     } else {
       if (i + 1 < ntile) patch();  // tile i+1, from the RGB bytes loaded during tile i-1's phase B
     }
+    C12_MARK(1);
     if (i == ntile) break;
     lds_reads_done();
     stage_barrier();  // B1: patch of tile i+1 complete; the partial tiles read
+    C12_MARK(2);
     if constexpr (TS == 0) {
       if (i + 1 < ntile) conv1(i + 1);
+      C12_MARK(3);
       stream(i);
+      C12_MARK(5);
     } else {
       if (i + 2 < ntile) rgb_load(i + 2);  // in flight during the stream
+      C12_MARK(4);
       stream(i);
       char* pp = part + cg * PART + lane * 16;
 #pragma unroll
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+      C12_MARK(5);
       if (i + 1 < ntile) conv1(i + 1);
+      C12_MARK(3);
     }
   }
+#ifdef NIC_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) o[q] = sx[q];
+    o[7] = ntile;
+  }
+#endif
+#undef C12_MARK
   range_report(a.rg, rmax);
 }
 

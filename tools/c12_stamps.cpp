@@ -1,7 +1,7 @@
-// Diagnostic harness (NOT part of the product): the fused conv1+conv2 kernel built with
+// Diagnostic harness (NOT part of the product): the pipelined conv1+conv2 kernel built with
 // NIC_STAMPS at the config-2 shape; per wave, cycle sums (s_memtime) per tile in: top
-// barrier, epilogue (ts 0) / colour patch (ts 1), patch barrier, conv1, RGB prefetch issue,
-// halo barrier, conv2 MFMAs + partials.  Build + run (GPU box):
+// barrier, epilogue (ts 0) / colour patch (ts 1), B1 barrier, conv1, RGB prefetch issue,
+// conv2 stream + partials.  Build + run (GPU box):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNIC_STAMPS \
 //     -I neural_network_image_compression_amd/csrc tools/c12_stamps.cpp -o /tmp/c12 && /tmp/c12
 #include "../neural_network_image_compression_amd/csrc/nic_kernels.hip"
@@ -82,7 +82,7 @@ int main() {
   CK(hipEventElapsedTime(&ms, e0, e1));
   std::vector<unsigned long long> hs((size_t)maxb * 64);
   CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
-  const char* nm[7] = {"top-bar", "epi/patch", "patch-bar", "conv1", "rgb-issue", "halo-bar", "mfma"};
+  const char* nm[7] = {"top-bar", "epi/patch", "B1-bar", "conv1", "rgb-issue", "stream", "other"};
   printf("conv12 %.4f ms\n", ms);
   for (int w = 0; w < 8; w += 4) {
     double s[7] = {}, nt = 0;
