@@ -300,7 +300,10 @@ def main():
             dec(enc(xh))
         hp = (time.perf_counter() - t0) / reps
         host_path = {"mp_per_s": round(B * H * W / 1e6 / hp, 1), "ms_per_batch": round(hp * 1e3, 3),
-                     "path": "Encoder()(numpy) -> Decoder()(numpy): host arrays through pinned staging, 4 chunks with H2D / device pass / D2H overlapped on two streams"}
+                     "path": "Encoder()(numpy) -> Decoder()(numpy) via nic_encode_host / nic_decode_host: "
+                             f"{Encoder.host_chunks} ramped chunks per call, H2D / device pass / D2H on three "
+                             "HIP streams; pageable input staged through pinned memory, results returned "
+                             "in page-locked arrays (the decoder DMAs the encoder's result directly)"}
     quality = None
     if args.workload in ("config2", "kodak") and min(H, W) >= 161:
         # device MS-SSIM (nic_ms_ssim) and PSNR (nic_sq_err) of the batch's reconstruction;

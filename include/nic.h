@@ -9,8 +9,8 @@
  *   Encoder()/Decoder() + ProClass.load(path)   nic_create + nic_set_weights
  *     encoder.py:34-36, decoder.py:35-37,
  *     utils.py:15-17, 26-28
- *   Encoder.__call__(x) encoder.py:38-47        nic_encode
- *   Decoder.__call__(z) decoder.py:39-48        nic_decode
+ *   Encoder.__call__(x) encoder.py:38-47        nic_encode (device) / nic_encode_host (NumPy)
+ *   Decoder.__call__(z) decoder.py:39-48        nic_decode (device) / nic_decode_host (NumPy)
  *   ProClass._feed_batch pack/unpack            nic_pack_latent / nic_unpack_latent
  *     utils.py:35-36, 39-40
  *   disc_entropy tf1_13/src/training.py:66-71   nic_entropy_hist
@@ -134,6 +134,17 @@ int nic_encode(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* l
  * rgb_f32 (nullable): the clipped fp32 RGB before round(x*255). */
 int nic_decode(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, float* rgb_f32,
                void* stream);
+
+/* Host-array surface: Encoder.__call__ / Decoder.__call__ on NumPy batches (encoder.py:38-47,
+ * decoder.py:39-48 hand host arrays in and out around every call).  rgb / latent are HOST
+ * pointers; the call is ordered after the work queued on `stream` and returns with the
+ * outputs written (synchronous).  The batch runs as `chunks` (1..16) chunks on the ctx's own
+ * streams, chunk k+1's H2D and chunk k-1's D2H overlapping chunk k's device pass; page-locked
+ * buffers are DMA'd directly, pageable ones staged through the ctx's pinned buffers. */
+int nic_encode_host(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, int chunks,
+                    void* stream);
+int nic_decode_host(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, int chunks,
+                    void* stream);
 
 /* Histogram entropy of each latent plane (tf1_13/src/training.py:66-71).
  * Plane order is the reference's concat along the batch: row p = plane p/n (Y,Cb,Cr) of

@@ -55,6 +55,8 @@ _SIGNATURES = {
                                         ctypes.POINTER(ctypes.c_int)]),
     "nic_encode": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_decode": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "nic_encode_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
+    "nic_decode_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
     "nic_entropy_hist": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_get_precision": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),

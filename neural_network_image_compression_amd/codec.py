@@ -171,6 +171,41 @@ class Codec:
         _lib.check(rc, "nic_decode")
         return (x, f) if rgb_f32 else x
 
+    # -- host entry points (NumPy u8 arrays; nic_encode_host / nic_decode_host) ----------
+    def _host_out(self, shape):
+        """A u8 result array in page-locked memory (torch's caching host allocator): the D2H
+        DMA lands in it directly, and a Decoder handed an Encoder result DMA's it directly."""
+        torch = _torch()
+        n = int(np.prod(shape))
+        return torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True).numpy()[:n].reshape(shape)
+
+    def encode_host(self, x: np.ndarray, chunks: int = 4) -> np.ndarray:
+        """(N,H,W,3) u8 host array -> (N,ceil(H/8),ceil(W/8),96) u8 host array (synchronous)."""
+        torch = _torch()
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        if x.ndim != 4 or x.shape[3] != 3:
+            raise ValueError(f"encode_host: expected shape (N,H,W,3), got {x.shape}")
+        n, h, w, _ = x.shape
+        h8, w8 = _lib.latent_shape(h, w) if h > 0 and w > 0 else (0, 0)
+        z = self._host_out((n, h8, w8, 96))
+        rc = self._L.nic_encode_host(self._h, x.ctypes.data, n, h, w, z.ctypes.data, int(chunks),
+                                     _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_encode_host")
+        return z
+
+    def decode_host(self, z: np.ndarray, chunks: int = 4) -> np.ndarray:
+        """(N,h,w,96) u8 host array -> (N,8h,8w,3) u8 host array (synchronous)."""
+        torch = _torch()
+        z = np.ascontiguousarray(z, dtype=np.uint8)
+        if z.ndim != 4 or z.shape[3] != 96:
+            raise ValueError(f"decode_host: expected shape (N,h,w,96), got {z.shape}")
+        n, h8, w8, _ = z.shape
+        x = self._host_out((n, 8 * h8, 8 * w8, 3))
+        rc = self._L.nic_decode_host(self._h, z.ctypes.data, n, h8, w8, x.ctypes.data, int(chunks),
+                                     _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_decode_host")
+        return x
+
     def entropy(self, z, counts: bool = False):
         """Histogram entropy per latent plane: (3N,) fp32 bits/symbol [, (3N,256) int32 counts]."""
         torch = _torch()
@@ -256,82 +291,11 @@ class Codec:
         return out
 
 
-class _HostPipe:
-    """Host-array surface of a device call: pinned staging buffers (grown on demand, reused)
-    and the batch cut into chunks so that chunk k's host->pinned copy and H2D DMA (copy
-    stream), chunk k-1's device pass (compute stream) and chunk k-2's D2H DMA overlap.
-    The reference's surface moves NumPy in and out around every call (encoder.py:38-47,
-    decoder.py:39-48); this is that hand-off, pipelined.  Every call synchronises before it
-    returns (NumPy out), so the staging buffers are free again for the next call."""
-
-    def __init__(self, device: int):
-        torch = _torch()
-        self.device = device
-        self.copy = torch.cuda.Stream(device)
-        self.comp = torch.cuda.Stream(device)
-        self._pin = {}
-
-    def _pinned(self, key: str, nbytes: int):
-        torch = _torch()
-        buf = self._pin.get(key)
-        if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
-            self._pin[key] = buf
-        return buf
-
-    def run(self, a: np.ndarray, fn, out_tail, chunks: int) -> np.ndarray:
-        """fn: device u8 (n, *a.shape[1:]) -> device u8 (n, *out_tail); returns NumPy."""
-        torch = _torch()
-        n = a.shape[0]
-        out = np.empty((n,) + tuple(out_tail), np.uint8)
-        if n == 0:
-            return out
-        a = np.ascontiguousarray(a)
-        in_row, out_row = a[0].nbytes, out[0].nbytes
-        pin_in = self._pinned("in", n * in_row)
-        pin_out = self._pinned("out", n * out_row)
-        cur = torch.cuda.current_stream(self.device)
-        self.copy.wait_stream(cur)  # the caller's earlier work on this device comes first
-        self.comp.wait_stream(cur)
-        bounds = np.linspace(0, n, min(chunks, n) + 1).astype(int)
-        done = []
-        keep = []
-        for lo, hi in zip(bounds[:-1], bounds[1:]):
-            if hi == lo:
-                continue
-            src = pin_in[lo * in_row:hi * in_row]
-            src.numpy()[:] = a[lo:hi].reshape(-1)  # host copy into pinned memory
-            with torch.cuda.stream(self.copy):
-                x = torch.empty((hi - lo,) + a.shape[1:], dtype=torch.uint8, device=f"cuda:{self.device}")
-                x.view(-1).copy_(src, non_blocking=True)
-                ev_in = torch.cuda.Event()
-                ev_in.record(self.copy)
-            with torch.cuda.stream(self.comp):
-                self.comp.wait_event(ev_in)
-                y = fn(x)
-                ev_y = torch.cuda.Event()
-                ev_y.record(self.comp)
-            with torch.cuda.stream(self.copy):
-                self.copy.wait_event(ev_y)
-                pin_out[lo * out_row:hi * out_row].copy_(y.reshape(-1), non_blocking=True)
-                ev_out = torch.cuda.Event()
-                ev_out.record(self.copy)
-            keep.append((x, y))  # device buffers stay alive until their DMA is done
-            done.append((lo, hi, ev_out))
-        flat = out.reshape(-1)
-        po = pin_out.numpy()
-        for lo, hi, ev in done:  # chunk k's pinned -> NumPy copy overlaps chunk k+1's work
-            ev.synchronize()
-            flat[lo * out_row:hi * out_row] = po[lo * out_row:hi * out_row]
-        cur.wait_stream(self.copy)
-        return out
-
-
 class ProClass:
     """utils.py:15-62: shared Y/CbCr model holder (kind 'encoder' or 'decoder')."""
 
-    #: chunks of the host-array pipeline (``_HostPipe``) per call
-    host_chunks = 4
+    #: chunks of the native host-array pipeline per call (nic_encode_host / nic_decode_host)
+    host_chunks = 3
 
     kind = ""
 
@@ -350,23 +314,19 @@ class ProClass:
     def _device_call(self, x):
         raise NotImplementedError
 
+    def _host_call(self, a: np.ndarray) -> np.ndarray:
+        raise NotImplementedError
+
     def __call__(self, x):
+        """Device tensors stay on the device; host arrays (NumPy, CPU tensors) go through the
+        native chunked host pipeline and come back as NumPy (in page-locked memory)."""
         torch = _torch()
         if isinstance(x, torch.Tensor) and x.device.type == "cuda":
             return self._device_call(x)
         a = _as_u8_array(x.cpu().numpy() if isinstance(x, torch.Tensor) else x, type(self).__name__)
         if a.ndim != 4:
             raise ValueError(f"{type(self).__name__}: expected a 4-D NHWC batch, got shape {a.shape}")
-        self._check_host(a)
-        if getattr(self, "_pipe", None) is None:
-            self._pipe = _HostPipe(self.codec.device)
-        return self._pipe.run(a, self._device_call, self._out_tail(a.shape), self.host_chunks)
-
-    def _check_host(self, a: np.ndarray) -> None:
-        pass
-
-    def _out_tail(self, shape):
-        raise NotImplementedError
+        return self._host_call(a)
 
 
 class Encoder(ProClass):
@@ -377,13 +337,10 @@ class Encoder(ProClass):
     def _device_call(self, x):
         return self.codec.encode(x)
 
-    def _check_host(self, a):
+    def _host_call(self, a):
         if a.shape[3] != 3:
             raise ValueError(f"Encoder: expected shape (N,H,W,3), got {a.shape}")
-
-    def _out_tail(self, shape):
-        h8, w8 = _lib.latent_shape(shape[1], shape[2])
-        return (h8, w8, 96)
+        return self.codec.encode_host(a, self.host_chunks)
 
     def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
         """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``.
@@ -402,12 +359,10 @@ class Decoder(ProClass):
     def _device_call(self, z):
         return self.codec.decode(z)
 
-    def _check_host(self, a):
+    def _host_call(self, a):
         if a.shape[3] != 96:
             raise ValueError(f"Decoder: expected shape (N,h,w,96), got {a.shape}")
-
-    def _out_tail(self, shape):
-        return (8 * shape[1], 8 * shape[2], 3)
+        return self.codec.decode_host(a, self.host_chunks)
 
     def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
         """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``."""

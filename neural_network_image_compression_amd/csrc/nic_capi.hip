@@ -252,6 +252,8 @@ struct DeviceGuard {
 
 }  // namespace
 
+constexpr int kHostMaxChunks = 16;
+
 struct nic_ctx {
   int device = 0;
   float* wk[L_COUNT] = {};  // [2 models][packed kernel]
@@ -279,6 +281,16 @@ struct nic_ctx {
   size_t qs_bytes = 0;
   // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
   // call, read back and accumulated by nic_layer_times
+  // host-array surface (nic_encode_host / nic_decode_host): its own copy-in, compute and
+  // copy-out streams, per-chunk events, pinned staging and device buffers, grown on demand
+  hipStream_t hs[3] = {};
+  hipEvent_t hev[3][kHostMaxChunks] = {};
+  hipEvent_t hev_caller = nullptr;
+  uint8_t* pin_in = nullptr;
+  uint8_t* pin_out = nullptr;
+  size_t pin_in_bytes = 0, pin_out_bytes = 0;
+  uint8_t* hdev = nullptr;
+  size_t hdev_bytes = 0;
   bool timing = false;
   hipEvent_t ev[L_COUNT][2] = {};
   bool ev_pending[L_COUNT] = {};
@@ -526,6 +538,15 @@ int nic_destroy(nic_ctx* c) {
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
+  for (int i = 0; i < 3; ++i) {
+    for (int k = 0; k < kHostMaxChunks; ++k)
+      if (c->hev[i][k]) (void)hipEventDestroy(c->hev[i][k]);
+    if (c->hs[i]) (void)hipStreamDestroy(c->hs[i]);
+  }
+  if (c->hev_caller) (void)hipEventDestroy(c->hev_caller);
+  if (c->pin_in) (void)hipHostFree(c->pin_in);
+  if (c->pin_out) (void)hipHostFree(c->pin_out);
+  if (c->hdev) (void)hipFree(c->hdev);
   delete c;
   return NIC_OK;
 }
@@ -824,6 +845,129 @@ int guarded(nic_ctx* c, hipStream_t st, const char* what, Pass pass) {
   return NIC_OK;
 }
 
+// -- host-array surface ------------------------------------------------------------------
+// Chunk k of a host call: its H2D DMA on hs[0], its device pass on hs[1], its D2H DMA on hs[2],
+// so chunk k+1's copy-in and chunk k-1's copy-out overlap chunk k's pass.  Chunk sizes ramp
+// up and down (weights min(2^i, 2^(K-1-i))): a small first chunk starts the device early and
+// a small last chunk keeps the exposed D2H tail short.
+void host_chunk_plan(int n, int k, std::vector<int>& lo) {
+  k = std::max(1, std::min({k, n, kHostMaxChunks}));
+  std::vector<double> wgt(k);
+  double tot = 0;
+  for (int i = 0; i < k; ++i) tot += wgt[i] = (double)(1 << std::min(i, k - 1 - i));
+  lo.assign(1, 0);
+  double acc = 0;
+  for (int i = 0; i < k; ++i) {
+    acc += wgt[i];
+    const int b = i + 1 == k ? n : std::max(lo.back() + 1, std::min(n - (k - 1 - i), (int)std::lround(n * acc / tot)));
+    lo.push_back(b);
+  }
+}
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // plain pageable memory: not known to HIP
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+int grow_pinned(uint8_t*& p, size_t& have, size_t need) {
+  if (need <= have) return NIC_OK;
+  if (p) HIP_TRY(hipHostFree(p));
+  p = nullptr;
+  have = 0;
+  if (hipHostMalloc((void**)&p, need, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(NIC_ENOMEM, "pinned staging allocation of %zu bytes failed", need);
+  }
+  have = need;
+  return NIC_OK;
+}
+
+int host_setup(nic_ctx* c) {
+  for (int i = 0; i < 3; ++i) {
+    if (!c->hs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking));
+    for (int k = 0; k < kHostMaxChunks; ++k)
+      if (!c->hev[i][k]) HIP_TRY(hipEventCreateWithFlags(&c->hev[i][k], hipEventDisableTiming));
+  }
+  if (!c->hev_caller) HIP_TRY(hipEventCreateWithFlags(&c->hev_caller, hipEventDisableTiming));
+  return NIC_OK;
+}
+
+// in (n x in_row bytes, host) -> pass(dev_in, count, dev_out, stream) per chunk -> out (host).
+// Page-locked inputs / outputs are DMA'd directly; pageable ones go through the ctx's pinned
+// staging (host memcpy of chunk k+1 while chunk k's DMA runs).  Ordered after the work
+// queued on `caller`; returns with every chunk's output in `out`.
+template <class Pass>
+int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, size_t out_row, int n, int chunks,
+                  hipStream_t caller, Pass pass) {
+  int rc = host_setup(c);
+  if (rc) return rc;
+  const bool in_pin = host_pinned(in), out_pin = host_pinned(out);
+  if (!in_pin && (rc = grow_pinned(c->pin_in, c->pin_in_bytes, n * in_row))) return rc;
+  if (!out_pin && (rc = grow_pinned(c->pin_out, c->pin_out_bytes, n * out_row))) return rc;
+  const size_t dev_bytes = ((n * in_row + 255) & ~(size_t)255) + n * out_row;
+  if (dev_bytes > c->hdev_bytes) {
+    if (c->hdev) HIP_TRY(hipFree(c->hdev));
+    c->hdev = nullptr;
+    c->hdev_bytes = 0;
+    if (hipMalloc(&c->hdev, dev_bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(NIC_ENOMEM, "host-surface device buffers of %zu bytes failed", dev_bytes);
+    }
+    c->hdev_bytes = dev_bytes;
+  }
+  uint8_t* d_in = c->hdev;
+  uint8_t* d_out = c->hdev + ((n * in_row + 255) & ~(size_t)255);
+  std::vector<int> lo;
+  host_chunk_plan(n, chunks, lo);
+  const int K = (int)lo.size() - 1;
+  HIP_TRY(hipEventRecord(c->hev_caller, caller));
+  HIP_TRY(hipStreamWaitEvent(c->hs[0], c->hev_caller, 0));
+  HIP_TRY(hipStreamWaitEvent(c->hs[1], c->hev_caller, 0));
+  int err = NIC_OK, issued = 0;
+  for (int k = 0; k < K && !err; ++k) {
+    const size_t i0 = lo[k] * in_row, ib = (lo[k + 1] - lo[k]) * in_row;
+    const size_t o0 = lo[k] * out_row, ob = (lo[k + 1] - lo[k]) * out_row;
+    const uint8_t* src = in + i0;
+    if (!in_pin) {
+      std::memcpy(c->pin_in + i0, in + i0, ib);
+      src = c->pin_in + i0;
+    }
+    hipError_t e = hipMemcpyAsync(d_in + i0, src, ib, hipMemcpyHostToDevice, c->hs[0]);
+    if (e == hipSuccess) e = hipEventRecord(c->hev[0][k], c->hs[0]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[1], c->hev[0][k], 0);
+    if (e != hipSuccess) {
+      err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
+      break;
+    }
+    err = pass(d_in + i0, lo[k + 1] - lo[k], d_out + o0, c->hs[1]);
+    if (err) break;
+    e = hipEventRecord(c->hev[1][k], c->hs[1]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[2], c->hev[1][k], 0);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(out_pin ? out + o0 : c->pin_out + o0, d_out + o0, ob, hipMemcpyDeviceToHost, c->hs[2]);
+    if (e == hipSuccess) e = hipEventRecord(c->hev[2][k], c->hs[2]);
+    if (e != hipSuccess) {
+      err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
+      break;
+    }
+    ++issued;
+  }
+  for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
+    hipError_t e = hipEventSynchronize(c->hev[2][k]);
+    if (e != hipSuccess) {
+      err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
+      break;
+    }
+    if (!out_pin) std::memcpy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
+  }
+  for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);  // drained on every path
+  return err;
+}
+
 }  // namespace
 
 extern "C" {
@@ -856,6 +1000,42 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   return guarded(c, st, "nic_decode", [&](bool x3, const RangeGuard& rg, bool timed) {
     return decode_pass(c, latent, n, h8, w8, rgb, rgb_f32, st, x3, rg, timed);
   });
+}
+
+int nic_encode_host(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, int chunks,
+                    void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_encode_host: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode_host: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode_host: encoder weights not fully set");
+  if (n == 0) return NIC_OK;
+  if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode_host: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode_host: batch %d exceeds 21845 images per call", n);
+  int h8, w8;
+  nic_latent_shape(h, w, &h8, &w8);
+  DeviceGuard guard(c->device);
+  return host_pipeline(c, rgb, (size_t)h * w * 3, latent, (size_t)h8 * w8 * 96, n, chunks, (hipStream_t)stream,
+                       [&](const uint8_t* x, int m, uint8_t* z, hipStream_t st) {
+                         return guarded(c, st, "nic_encode_host", [&](bool x3, const RangeGuard& rg, bool timed) {
+                           return encode_pass(c, x, m, h, w, z, nullptr, st, x3, rg, timed);
+                         });
+                       });
+}
+
+int nic_decode_host(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t* rgb, int chunks,
+                    void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_decode_host: NULL ctx");
+  if (n < 0 || h8 <= 0 || w8 <= 0) return fail(NIC_ESHAPE, "nic_decode_host: bad latent shape (%d,%d,%d,96)", n, h8, w8);
+  if (!models_ready(c, 2)) return fail(NIC_ENOWEIGHTS, "nic_decode_host: decoder weights not fully set");
+  if (n == 0) return NIC_OK;
+  if (!latent || !rgb) return fail(NIC_EINVAL, "nic_decode_host: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_decode_host: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  return host_pipeline(c, latent, (size_t)h8 * w8 * 96, rgb, (size_t)64 * h8 * w8 * 3, n, chunks, (hipStream_t)stream,
+                       [&](const uint8_t* z, int m, uint8_t* x, hipStream_t st) {
+                         return guarded(c, st, "nic_decode_host", [&](bool x3, const RangeGuard& rg, bool timed) {
+                           return decode_pass(c, z, m, h8, w8, x, nullptr, st, x3, rg, timed);
+                         });
+                       });
 }
 
 int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,

@@ -3053,6 +3053,17 @@ __global__ __launch_bounds__(256) void unpack_latent_kernel(const uint8_t* __res
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
+// Grid of a grid-stride fp32 kernel: 8 blocks per CU, but one per CU for the gated re-run of
+// the range-guard fallback, which exits at once unless its pass tripped (the usual case: a
+// smaller grid drains faster; a tripped pass re-runs on fewer, longer-lived blocks)
+static int fp32_grid(const RangeGuard& rg, long long jobs) {
+  static const int gated_per_cu = [] {
+    const char* e = std::getenv("NIC_GATE_GRID");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  return (int)std::min<long long>(jobs, (long long)(rg.gate ? gated_per_cu : 8) * device_cus());
+}
+
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
           int OUT_MODE, bool RESID>
 static hipError_t launch_conv(ConvArgs a, hipStream_t st) {
@@ -3062,7 +3073,7 @@ static hipError_t launch_conv(ConvArgs a, hipStream_t st) {
   const long long jobs = (long long)a.tiles_y * a.tiles_x * a.P;
   if (jobs == 0) return hipSuccess;
   if (jobs > INT32_MAX) return hipErrorInvalidValue;
-  const int grid = (int)std::min<long long>(jobs, 8LL * device_cus());
+  const int grid = fp32_grid(a.rg, jobs);
   hipLaunchKernelGGL((conv_mfma_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>),
                      dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
@@ -3268,7 +3279,7 @@ hipError_t launch_conv1(Conv1Args a, hipStream_t st) {
   const long long jobs = (long long)a.tiles_y * a.tiles_x * a.P;
   if (jobs == 0) return hipSuccess;
   if (jobs > INT32_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv1_colour_kernel, dim3((int)std::min<long long>(jobs, 8LL * device_cus())), dim3(256), 0,
+  hipLaunchKernelGGL(conv1_colour_kernel, dim3(fp32_grid(a.rg, jobs)), dim3(256), 0,
                      st, a);
   return hipGetLastError();
 }
@@ -3279,7 +3290,7 @@ hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
   const long long jobs = (long long)a.tiles_y * a.tiles_x * a.nimg;
   if (jobs == 0) return hipSuccess;
   if (jobs > INT32_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dconv8_colour_kernel, dim3((int)std::min<long long>(jobs, 8LL * device_cus())), dim3(256), 0,
+  hipLaunchKernelGGL(dconv8_colour_kernel, dim3(fp32_grid(a.rg, jobs)), dim3(256), 0,
                      st, a);
   return hipGetLastError();
 }

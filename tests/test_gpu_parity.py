@@ -296,6 +296,19 @@ def test_numpy_surface_matches_device(codecs, golden, weights_spread):
     assert np.array_equal(z, codecs["spread"].encode(_dev(g["x"])).cpu().numpy())
     r = dec(z)
     assert r.shape == (4, 128, 128, 3)
+    assert np.array_equal(r, codecs["spread"].decode(_dev(z)).cpu().numpy())
+    # the host pipe: z is a view of page-locked memory (DMA'd directly by the decoder); a
+    # pageable copy of it (staged), a read-only one and odd chunkings give the same bytes
+    assert torch.from_numpy(z.reshape(-1)).is_pinned()
+    z_page = z.copy()
+    z_ro = z.copy()
+    z_ro.setflags(write=False)
+    for chunks in (1, 3, 7):
+        dec.host_chunks = chunks
+        assert np.array_equal(dec(z_page), r) and np.array_equal(dec(z_ro), r)
+    z0 = z.copy()
+    z2 = enc(g["x"][::-1].copy())  # a second call returns a fresh buffer, the first is intact
+    assert np.array_equal(z2, z0[::-1]) and np.array_equal(z, z0)
     with pytest.raises(ValueError):
         enc(g["x"][0])  # 3-D input
     with pytest.raises(ValueError):
