@@ -57,6 +57,8 @@ def test_null_arguments_are_rejected_without_crashing():
     assert L.nic_encode(None, None, 1, 8, 8, None, None, None) == _lib.NIC_EINVAL
     assert "NULL" in _lib.last_error()
     assert L.nic_decode(None, None, 1, 1, 1, None, None, None) == _lib.NIC_EINVAL
+    assert L.nic_encode_host(None, None, 1, 8, 8, None, 3, None) == _lib.NIC_EINVAL
+    assert L.nic_decode_host(None, None, 1, 1, 1, None, 3, None) == _lib.NIC_EINVAL
     assert L.nic_set_weights(None, 0, b"conv1/kernel", None, None, 0) == _lib.NIC_EINVAL
     assert L.nic_pack_latent(None, 1, 1, 1, None, None) == _lib.NIC_EINVAL
     assert L.nic_pack_latent(None, 1, 0, 1, None, None) == _lib.NIC_ESHAPE
