@@ -159,6 +159,39 @@ def cpu_baseline(weights, size: int, seconds: float, batch: int = 4):
                       f"CPU restatement of tf2_0, not TF2 (not installable), {el:.1f} s"}
 
 
+def power_probe(device, weights, x, z, r, dom, flop, steps, peak):
+    """The dominant kernel's rate with every weight zero (a second codec on the same GPU, same
+    kernels, same launch shapes): the MFMA operands are then all zero and the chip holds a
+    higher clock.  Same cycles, different clock -- the gap between `frac` and this figure is
+    the data-dependent MFMA power the split-f16 pass draws (DVFS), not scheduling."""
+    import torch
+
+    from neural_network_image_compression_amd.codec import Codec
+
+    zw = {k: np.zeros_like(v) for k, v in weights.items()}
+    c = Codec(device)
+    c.set_weights(zw)
+    c.reserve(*x.shape[:3])
+    for _ in range(10):
+        c.encode(x, out=z)
+        c.decode(z, out=r)
+    c.set_timing(True)
+    for _ in range(steps):
+        c.encode(x, out=z)
+        c.decode(z, out=r)
+    lt = c.layer_times()
+    c.set_timing(False)
+    torch.cuda.synchronize()
+    ms, n = lt[dom]
+    avg = ms / max(n, 1)
+    tf = flop / (avg * 1e-3) / 1e12
+    per_layer = {k: round(v[0] / v[1], 4) for k, v in lt.items() if v[1] > 0}
+    return {"zero_operand_avg_ms": round(avg, 4), "zero_operand_tflops": round(tf, 2),
+            "zero_operand_frac": round(tf / peak, 4), "zero_operand_layer_ms": per_layer,
+            "note": "same kernels with all-zero weights (zero MFMA operands): the chip clocks higher "
+                    "(DVFS); frac below this is the power limit of random-data split-f16 MFMAs"}
+
+
 def parity_sample(codec, x0, weights):
     """PSNR of the GPU reconstruction of one benchmarked image vs the oracle's (fp64 acc)."""
     import torch
@@ -197,6 +230,7 @@ def main():
                     help="arithmetic of the Cin>=32 convolutions (see include/nic.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-power-probe", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-layer HBM bytes per launch from the rocprofv3 PMC pass")
     args = ap.parse_args()
@@ -434,6 +468,8 @@ def main():
         out["cpu_baseline"]["numpy_oracle"] = cpu_baseline_numpy(weights, S, args.cpu_seconds / 2)
     if not args.no_parity and args.workload == "config2":
         out["parity"] = parity_sample(codec, x[:1], weights)
+    if not args.no_power_probe and args.workload == "config2" and args.precision == "f16x3":
+        out["roofline"]["power_probe"] = power_probe(local, weights, x, z, r, dom, flops[dom], args.steps, peak)
     print(json.dumps(out), flush=True)
     barrier()
     if world > 1:

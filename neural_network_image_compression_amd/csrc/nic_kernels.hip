@@ -1196,9 +1196,15 @@ struct GeomWS {
 // sum_ci h[px][ci] w8[tap][ci] on the same split-f16 MFMA (2 tap blocks x 2 k32-steps x 3,
 // B fragments from an LDS copy of w8), scaled by 2^-k8 and stored tile-major (a.proj).
 // One extra barrier per tile (hproj complete); the next tile's barrier orders its reuse.
+// diagnostic build only: no projection MFMAs / stores in dconv7 (wrong results)
+#ifdef NIC_DIAG_NOPROJ
+constexpr bool kProjOff = true;
+#else
+constexpr bool kProjOff = false;
+#endif
 template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP, bool PROJ = false>
 __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
-                                        int px) {
+                                        int px, bool copy_w8 = true) {
   constexpr int NTAPS = KH * KW, NW = COUT / 16, KST = CIN / 32, MT = TH * TW / 16;
   static_assert(TW == 8 && CIN % 32 == 0 && COUT % 16 == 0, "16-pixel tiles = two 8-pixel rows");
   static_assert(!(TRP && RESID), "no residual on the transposed phases");
@@ -1245,10 +1251,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   const f16x8* w8lds = (const f16x8*)(lds + 2 * G::HALO_BYTES) + lane;
   const float scale8 = PROJ ? a.proj_scale[model] : 0.f;
   char* hproj = lds + 2 * G::HALO_BYTES + W8F * 64 * 16;
-  if constexpr (PROJ) {
-    const f16x8* src = (const f16x8*)a.proj_w + (size_t)model * W8F * 64;
-    for (int q = threadIdx.x; q < W8F * 64; q += 64 * NW) ((f16x8*)(lds + 2 * G::HALO_BYTES))[q] = src[q];
-  }
+  if constexpr (PROJ)
+    if (copy_w8) {
+      const f16x8* src = (const f16x8*)a.proj_w + (size_t)model * W8F * 64;
+      for (int q = threadIdx.x; q < W8F * 64; q += 64 * NW) ((f16x8*)(lds + 2 * G::HALO_BYTES))[q] = src[q];
+    }
 
   // B fragments: pixel (2m + l16/8 + kh, l16%8 + kw), chunk c = 8 hl + 4 ks + g in slot
   // c ^ swz(l16%8 + kw).  bx[kw] = record address (m = kh = 0) | slot of chunk g; chunk
@@ -1292,6 +1299,45 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
   int ep_p = 0, ep_y = 0, ep_x = 0;  // tile whose epilogue is pending
   float rmax = 0.f;                  // range guard of the split output
+  // PROJ: tile i-1's projection, 4 chunks (tap block nt, k32-step ks) of 3 MFMAs, runs
+  // between the projection barrier and tile i's stream.  (Interleaving the chunks into tile
+  // i's MFMA stream, stores deferred past the next barrier, measured 2 % slower.)
+  f32x4 pd[2];  // projections (tap block nt)
+  // one k32-step of A fragments (tile pixels) and one chunk of w8 live at a time
+  f16x8 pah, pal, pwh, pwl;
+  const int ppx = 16 * wave + l16;  // projected pixel of this lane's A rows
+  auto proj_load_a = [&](int ks) {
+    pah = *(const f16x8*)(hproj + ppx * 256 + (((4 * ks + g) ^ (ppx & 15)) << 4));
+    pal = *(const f16x8*)(hproj + ppx * 256 + (((8 + 4 * ks + g) ^ (ppx & 15)) << 4));
+  };
+  auto proj_load_w = [&](int j) {  // chunk j: nt = j & 1, ks = j >> 1
+    pwh = w8lds[(((j & 1) * KST + (j >> 1)) * 2 + 0) * 64];
+    pwl = w8lds[(((j & 1) * KST + (j >> 1)) * 2 + 1) * 64];
+  };
+  auto proj_mfma = [&](int j) {
+    f32x4& d = pd[j & 1];
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(pal, pwh, d, 0, 0, 0);  // a_lo*w_hi
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(pah, pwl, d, 0, 0, 0);  // a_hi*w_lo
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(pah, pwh, d, 0, 0, 0);  // a_hi*w_hi
+  };
+  // chunks in the order (nt, ks) = (0,0), (1,0), (0,1), (1,1); after chunk j the next one's
+  // fragments are read (its A at the k32-step change)
+  auto proj_chunk = [&](int j) {
+    proj_mfma(j);
+    if (j == 1) proj_load_a(1);
+    if (j + 1 < 4) proj_load_w(j + 1);
+  };
+  auto proj_store = [&](float* dst) {  // lane (g, l16): pixels 16w + 4g .. +3 of tap 16nt + l16
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int tap = 16 * nt + l16;
+      if (tap < 25) *(f32x4*)(dst + tap * 64) = pd[nt] * scale8;
+    }
+  };
+  auto proj_dst = [&] {  // a.proj block of the tile whose epilogue just ran (ep_*)
+    return a.proj + ((((size_t)ep_p * 4 + 2 * py + px) * a.tiles_y + ep_y / TH) * a.tiles_x + ep_x / TW) * (25 * 64) +
+           16 * wave + 4 * g;
+  };
 #ifdef NIC_STAMPS
   unsigned long long s_wait = 0, s_epi = 0, s_mfma = 0, s_t0, s_t1, s_t2;
   const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
@@ -1340,7 +1386,6 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         }
       }
     }
-    f16x8 ah[KST], al[KST];
     // PROJ: the next halo's DMA issue runs before the projection barrier, where it overlaps
     // the other waves finishing their epilogues (buffer (i+1)&1 was last read by tile i-1's
     // stream, which every wave finished before the top barrier)
@@ -1352,42 +1397,17 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #ifndef NIC_DIAG_NOBAR2  // diagnostic build: no projection barrier (racy, wrong results)
         stage_barrier();   // the whole tile's channels are in hproj
 #endif
-        const int pp = 16 * wave + l16;
-#pragma unroll
-        for (int ks = 0; ks < KST; ++ks) {
-          ah[ks] = *(const f16x8*)(hproj + pp * 256 + (((4 * ks + g) ^ (pp & 15)) << 4));
-          al[ks] = *(const f16x8*)(hproj + pp * 256 + (((8 + 4 * ks + g) ^ (pp & 15)) << 4));
-        }
       }
     if constexpr (!PROJ)
       if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
-    if constexpr (PROJ)
-      if (i > 0) {
-        float* dst = a.proj +
-                     ((((size_t)ep_p * 4 + 2 * py + px) * a.tiles_y + ep_y / TH) * a.tiles_x + ep_x / TW) * (25 * 64) +
-                     16 * wave + 4 * g;
-#ifndef NIC_DIAG_NOPROJ  // diagnostic build: no projection MFMAs / stores (wrong results)
+    if constexpr (PROJ && !kProjOff)
+      if (i > 0) {  // tile i-1's projection (4 chunks of 3 MFMAs) and its stores
+        proj_load_a(0);
+        proj_load_w(0);
+        pd[0] = pd[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-#else
-        for (int nt = 0; nt < 0; ++nt) {
-#endif
-          f16x8 wh[KST], wl[KST];
-#pragma unroll
-          for (int ks = 0; ks < KST; ++ks) {
-            wh[ks] = w8lds[((nt * KST + ks) * 2 + 0) * 64];
-            wl[ks] = w8lds[((nt * KST + ks) * 2 + 1) * 64];
-          }
-          f32x4 d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < KST; ++ks) {
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[ks], wh[ks], d, 0, 0, 0);  // a_lo*w_hi
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], wl[ks], d, 0, 0, 0);  // a_hi*w_lo
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], wh[ks], d, 0, 0, 0);  // a_hi*w_hi
-          }
-          const int tap = 16 * nt + l16;
-          if (tap < 25) *(f32x4*)(dst + tap * 64) = d * scale8;
-        }
+        for (int j = 0; j < 4; ++j) proj_chunk(j);
+        proj_store(proj_dst());
       }
     if (i == ntile) break;
     tile_at(i, ep_p, ep_y, ep_x);
@@ -2212,6 +2232,14 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
   const int model = gi & 1;
   if constexpr (!TRP) {
     ws_body<CIN, COUT, TH, TW, RESID, 3, 3, false>(a, lds, model, bi, nb, 0, 0, 0);
+  } else if (a.ws_ngrp == 2) {
+    // every block runs all four sub-pixel phases over its share of the model's tiles, one
+    // after the other (weights reloaded per phase; dconv8's w8 copied to LDS once): equal
+    // work per block whatever the per-tile overheads of the phases
+    ws_body<CIN, COUT, TH, TW, false, 3, 3, true, PROJ>(a, lds, model, bi, nb, 16, 1, 1);
+    ws_body<CIN, COUT, TH, TW, false, 2, 3, true, PROJ>(a, lds, model, bi, nb, 4, 0, 1, false);
+    ws_body<CIN, COUT, TH, TW, false, 3, 2, true, PROJ>(a, lds, model, bi, nb, 10, 1, 0, false);
+    ws_body<CIN, COUT, TH, TW, false, 2, 2, true, PROJ>(a, lds, model, bi, nb, 0, 0, 0, false);
   } else {
     switch (gi >> 1) {  // phase-major tap bases 0, 4, 10, 16 (for_each_phase_tap)
       case 0: ws_body<CIN, COUT, TH, TW, false, 2, 2, true, PROJ>(a, lds, model, bi, nb, 0, 0, 0); break;
@@ -3159,6 +3187,26 @@ static int ws_k3_blocks_per_cu() {
   return v;
 }
 
+// Per-tile cost of the dconv7 phase groups beyond their MFMA work, in units of half a tap
+// (the projection's 12 MFMAs are one unit; the epilogue, halo issue and barriers add the
+// rest); NIC_D7_C overrides for A/B runs.
+static int ws_proj_cost() {
+  static const int v = [] {
+    const char* e = getenv("NIC_D7_C");
+    const int n = e ? atoi(e) : 1;
+    return n >= 0 && n <= 64 ? n : 1;
+  }();
+  return v;
+}
+
+static bool d7_grouped() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_D7");
+    return e && e[0] == 'g';
+  }();
+  return on;
+}
+
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
 // in proportion to each group's MFMA work (planes x taps).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
@@ -3172,14 +3220,16 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   // HaloDma: 32-bit plane offsets, out-of-range slots past the plane (kDmaOOR)
   if ((long long)a.H * a.W * CIN * 4 >= (1LL << 30)) return hipErrorInvalidValue;
   a.ntiles = (int)nt;
-  const int nset = TRP ? 4 : 1;
-  const int taps[4] = {TRP ? 4 : 9, 6, 6, 9};
+  // transposed layers: one block group per model, every block runs the four phases
+  // (default), or per-phase groups (NIC_D7=g, A/B)
+  const int nset = TRP && d7_grouped() ? 4 : 1;
+  const int taps[4] = {TRP ? (nset == 4 ? 4 : 25) : 9, 6, 6, 9};
   a.ws_taps = TRP ? 25 : 9;
   a.ws_ngrp = 2 * nset;
   long long work[8], total = 0;
   for (int gi = 0; gi < a.ws_ngrp; ++gi) {
     const long long planes = (gi & 1) ? a.P - a.nimg : a.nimg;
-    work[gi] = planes * per_plane * (2 * taps[gi >> 1] + (PROJ ? 1 : 0));  // + projection: 12 of 24/tap MFMAs
+    work[gi] = planes * per_plane * (2 * taps[gi >> 1] + (PROJ ? ws_proj_cost() : 0));
     total += work[gi];
   }
   const int target = (TRP ? 2 : ws_k3_blocks_per_cu()) * device_cus();
