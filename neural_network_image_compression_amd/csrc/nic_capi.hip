@@ -263,7 +263,8 @@ struct nic_ctx {
   // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
   uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
-  // f16 range guard (nic.h NIC_RANGE_*): device words [flag, re-run count], the epoch of the
+  // f16 range guard (nic.h NIC_RANGE_*): device words [flag, re-run count, and the chained
+  // re-run's grid-barrier pair], the epoch of the
   // latest split-f16 pass, the policy, a pinned host word for the ERROR policy's check
   int* range = nullptr;
   int* range_host = nullptr;
@@ -494,7 +495,7 @@ int nic_create(int device, nic_ctx** out) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
   }
-  if (hipMalloc(&c->range, 2 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 2 * sizeof(int)) != hipSuccess ||
+  if (hipMalloc(&c->range, 4 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 4 * sizeof(int)) != hipSuccess ||
       hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: range-guard allocation failed");
@@ -634,6 +635,15 @@ int nic_reserve(nic_ctx* c, int n, int h, int w) {
 
 namespace {
 
+// NIC_CHAIN=0: the gated re-run as one launch per layer (A/B)
+bool use_chain() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_CHAIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // One encode pass: split-f16 kernels (x3, producers report to rg.flag) or exact-fp32 ones
 // (rg.gate set: a re-run that exits unless the split pass of the same epoch tripped).
 // `timed` brackets the launches with the per-layer events (the gated re-run is not timed).
@@ -667,13 +677,20 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   a1.OW = g.c1x.out;
   a1.pad_y = g.c1y.lo;
   a1.pad_x = g.c1x.lo;
+  // the gated exact-fp32 re-run: all layers recorded into one cooperative launch
+  Fp32Chain chain{};
+  const bool chained = !x3 && rg.gate && use_chain();
+  chain.gate = rg;
+  chain.bar = c->range + 2;
   // f16x3: conv1 runs inside the conv2 kernel (launch_conv12_x3, timed as conv2)
   const bool fuse12 = x3 && conv12_fused();
-  if (!fuse12) TIMED(L_CONV1, launch_conv1(a1, st));
+  if (!fuse12) TIMED(L_CONV1, chained ? chain_add_conv1(chain, a1) : launch_conv1(a1, st));
   // the re-run's head is conv1 (it counts the trip); later layers only gate
   RangeGuard rgl = rg;
   rgl.trips = nullptr;
-  auto run = [&](LayerId id, const ConvArgs& a) { return x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st); };
+  auto run = [&](LayerId id, const ConvArgs& a) {
+    return chained ? chain_add_layer(chain, id, a) : x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st);
+  };
 
   auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW, int py,
                   int px) {
@@ -723,6 +740,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   a8.out_u8 = latent;
   a8.out_f32_latent = prequant;
   TIMED(L_CONV8, run(L_CONV8, a8));
+  if (chained) HIP_TRY(launch_fp32_chain(chain, st));
   return NIC_OK;
 }
 
@@ -744,7 +762,13 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   // the re-run's head is dconv1 (it counts the trip); later layers only gate
   RangeGuard rgl = rg;
   rgl.trips = nullptr;
-  auto run = [&](LayerId id, const ConvArgs& a) { return x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st); };
+  Fp32Chain chain{};  // the gated exact-fp32 re-run as one cooperative launch (see encode_pass)
+  const bool chained = !x3 && rg.gate && use_chain();
+  chain.gate = rg;
+  chain.bar = c->range + 2;
+  auto run = [&](LayerId id, const ConvArgs& a) {
+    return chained ? chain_add_layer(chain, id, a) : x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st);
+  };
   auto conv = [&](LayerId id, const float* in, float* out, const float* res, int H, int W, int OH, int OW) {
     ConvArgs a{};
     a.rg = rgl;
@@ -810,8 +834,9 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
     a8.tiles_x7 = (w2 + 7) / 8;
     TIMED(L_DCONV8, launch_dconv8_gather(a8, st));
   } else {
-    TIMED(L_DCONV8, x3 ? launch_dconv8_x3(a8, st) : launch_dconv8(a8, st));
+    TIMED(L_DCONV8, x3 ? launch_dconv8_x3(a8, st) : chained ? chain_add_dconv8(chain, a8) : launch_dconv8(a8, st));
   }
+  if (chained) HIP_TRY(launch_fp32_chain(chain, st));
   return NIC_OK;
 }
 

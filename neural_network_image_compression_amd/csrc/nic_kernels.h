@@ -95,6 +95,23 @@ struct Dconv8Args {
   int tiles_y7, tiles_x7;      // gather kernel: dconv7's 8x8 tile grid over its coarse input
 };
 
+// The gated exact-fp32 re-run of a split-f16 pass as one cooperative launch (stages run in
+// order with grid barriers; every block exits at once unless gate.gate == gate.epoch).
+constexpr int kChainMax = 6;
+struct Fp32Chain {
+  RangeGuard gate;  // gate + trips of the re-run (the stages' own rg fields are unused)
+  int* bar;         // 2 zeroed device words: barrier arrivals, generation
+  int nstage;
+  int kind[kChainMax];      // LayerId; L_CONV1 -> c1, L_DCONV8 -> d8, other layers -> c[s]
+  ConvArgs c[kChainMax];
+  Conv1Args c1;
+  Dconv8Args d8;
+};
+hipError_t chain_add_layer(Fp32Chain& ch, LayerId id, ConvArgs a);
+hipError_t chain_add_conv1(Fp32Chain& ch, Conv1Args a);
+hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a);
+hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st);
+
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA

@@ -232,16 +232,15 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, int p, int model, 
   }
 }
 
+// Body of one block (b0 of nb) over its (plane, tile) jobs, grid-stride; `lds` holds
+// G::LDS_FLOATS floats.  Called by conv_mfma_kernel and by the chained gated re-run
+// (fp32_chain_kernel).
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
           int OUT_MODE, bool RESID>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_mfma_body(const ConvArgs& a, float* lds, int b0, int nb) {
   using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
-  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-  if (range_gated_off(a.rg)) return;
-  // grid-stride over (plane, tile) jobs: a capped grid, so that a gated launch that has
-  // nothing to do (the f16x3 pass it backs up stayed in range) costs one small dispatch
   const int per_plane = a.tiles_y * a.tiles_x;
-  for (int job = blockIdx.x; job < per_plane * a.P; job += gridDim.x) {
+  for (int job = b0; job < per_plane * a.P; job += nb) {
   __syncthreads();  // every wave is done with the previous job's LDS
   const int p = job / per_plane;
   const int tile = job - p * per_plane;
@@ -410,6 +409,14 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     }
   }
   }  // job
+}
+
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
+          int OUT_MODE, bool RESID>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+  using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
+  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+  conv_mfma_body<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>(a, lds, blockIdx.x, gridDim.x);
 }
 
 
@@ -2133,6 +2140,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   if (ntile > 0) conv1(0);
 #ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
   unsigned long long sx[8] = {}, sa, sb;
+  const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
   NIC_PNOW(sa);
 #define C12_MARK(kk)   \
   do {                 \
@@ -2183,6 +2191,10 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
 #pragma unroll
     for (int q = 0; q < 7; ++q) o[q] = sx[q];
     o[7] = ntile;
+    if (wave == 0) {  // shader clock: cycles and 100 MHz ticks of the loop, after the stamp area
+      g_stamps[256 * 64 + 2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - s_c0;
+      g_stamps[256 * 64 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - s_rt0;
+    }
   }
 #endif
 #undef C12_MARK
@@ -2263,12 +2275,11 @@ constexpr int C1_HE = (C1_HH + 1) / 2;     // 18 even columns, then 17 odd ones
 // consecutive -- conflict-free ds_read_b32 for all 32 lanes of a half
 constexpr int C1_PS = 40;
 
-__global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
-  __shared__ float plane[C1_HH * C1_PS];
-  if (range_gated_off(a.rg)) return;
+constexpr int C1_LDS_FLOATS = C1_HH * C1_PS;
+__device__ __forceinline__ void conv1_colour_body(const Conv1Args& a, float* plane, int b0, int nb) {
   float rmax = 0.f;  // range guard of the split output
   const int per_plane = a.tiles_y * a.tiles_x;
-  for (int job = blockIdx.x; job < per_plane * a.P; job += gridDim.x) {  // capped grid, as conv_mfma
+  for (int job = b0; job < per_plane * a.P; job += nb) {  // grid-stride, as conv_mfma
   __syncthreads();  // the previous job's plane reads are done
   const int p = job / per_plane, tile = job - p * per_plane;
   const int n = p % a.nimg, type = p / a.nimg;
@@ -2367,6 +2378,12 @@ __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
   range_report(a.rg, rmax);
 }
 
+__global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
+  __shared__ float plane[C1_LDS_FLOATS];
+  if (range_gated_off(a.rg)) return;
+  conv1_colour_body(a, plane, blockIdx.x, gridDim.x);
+}
+
 // ------------------------------------------------------------------------------------
 // dconv8 (64 -> 1, transposed k5 s2) fused with the inverse colour transform and output
 // quantiser (decoder.py:31-32, 45-48; utils.py:70-72).  HBM-bound: it streams the 64-ch
@@ -2434,11 +2451,10 @@ __device__ __forceinline__ void d8_store_rgb(const Dconv8Args& a, int n, int my,
   }
 }
 
-__global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
-  __shared__ __attribute__((aligned(16))) float halo[D8_HH * D8_HW * D8_PS];
-  if (range_gated_off(a.rg)) return;
+constexpr int D8_LDS_FLOATS = D8_HH * D8_HW * D8_PS;
+__device__ __forceinline__ void dconv8_colour_body(const Dconv8Args& a, float* halo, int b0, int nb) {
   const int per_img = a.tiles_y * a.tiles_x;
-  for (int job = blockIdx.x; job < per_img * a.nimg; job += gridDim.x) {  // capped grid, as conv_mfma
+  for (int job = b0; job < per_img * a.nimg; job += nb) {  // grid-stride, as conv_mfma
   const int n = job / per_img, tile = job - n * per_img;
   const int tyi = tile / a.tiles_x;
   const int t0y = tyi * D8_TH, t0x = (tile - tyi * a.tiles_x) * D8_TW;
@@ -2503,6 +2519,12 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
   const int my = t0y + ty, mx = t0x + tx;
   if (my < a.H && mx < a.W) d8_store_rgb(a, n, my, mx, outv);
   }  // job (the next job's first step barrier orders the halo reuse)
+}
+
+__global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
+  __shared__ __attribute__((aligned(16))) float halo[D8_LDS_FLOATS];
+  if (range_gated_off(a.rg)) return;
+  dconv8_colour_body(a, halo, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3084,11 +3106,124 @@ __global__ __launch_bounds__(256) void unpack_latent_kernel(const uint8_t* __res
 // Grid of a grid-stride fp32 kernel: 8 blocks per CU, but one per CU for the gated re-run of
 // the range-guard fallback, which exits at once unless its pass tripped (the usual case: a
 // smaller grid drains faster; a tripped pass re-runs on fewer, longer-lived blocks)
+// ------------------------------------------------------------------------------------
+// The gated exact-fp32 re-run of a split-f16 pass as ONE launch: every stage of the pass
+// (conv1 / conv_mfma layers / dconv8) in sequence, a grid barrier between stages.  When
+// the split pass stayed in range every block exits at the gate, so the pass costs one
+// dispatch instead of one per layer (each dispatch, even of an empty kernel, holds the
+// queue for ~5 us: measured 4.7-5.3 us for 1 to 256 blocks).  Cooperative launch, one
+// block per CU (all resident, as the barrier needs).
+// ------------------------------------------------------------------------------------
+template <class... Gs>
+constexpr int max_lds_floats() {
+  int m = 0;
+  ((m = Gs::LDS_FLOATS > m ? Gs::LDS_FLOATS : m), ...);
+  return m;
+}
+using G_c2 = ConvGeom<32, 64, 5, 2, false, 8, 8, 2, 2, 1>;
+using G_k3 = ConvGeom<64, 64, 3, 1, false, 8, 16, 4, 1, 1>;
+using G_c8 = ConvGeom<64, 32, 5, 2, false, 4, 8, 1, 1, 4>;
+using G_d1 = ConvGeom<32, 64, 5, 2, true, 8, 8, 2, 2, 1>;
+using G_d7 = ConvGeom<64, 64, 5, 2, true, 8, 16, 4, 1, 1>;
+constexpr int kChainLds = std::max({max_lds_floats<G_c2, G_k3, G_c8, G_d1, G_d7>(), C1_LDS_FLOATS, D8_LDS_FLOATS});
+
+// grid barrier over nb blocks: bar[0] arrivals (back to 0 after every barrier), bar[1]
+// generation.  Vector atomics and agent-scope fences (stage outputs visible across XCDs).
+__device__ __forceinline__ void grid_barrier(int* bar, int nb) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();  // release this block's stage outputs
+    if (atomicAdd(bar, 1) == nb - 1) {
+      __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      atomicAdd(bar + 1, 1);
+    } else {
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence();  // acquire the other blocks' outputs
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void fp32_chain_kernel(Fp32Chain ch) {
+  __shared__ __attribute__((aligned(16))) float lds[kChainLds];
+  if (range_gated_off(ch.gate)) return;  // whole grid: the gate word is the same for every block
+  const int b0 = blockIdx.x, nb = gridDim.x;
+  for (int s = 0; s < ch.nstage; ++s) {
+    if (s > 0) grid_barrier(ch.bar, nb);
+    const ConvArgs& a = ch.c[s];
+    switch (ch.kind[s]) {
+      case L_CONV1: conv1_colour_body(ch.c1, lds, b0, nb); break;
+      case L_DCONV8: dconv8_colour_body(ch.d8, lds, b0, nb); break;
+      case L_CONV2: conv_mfma_body<32, 64, 5, 2, false, 8, 8, 2, 2, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_CONV3:
+      case L_DCONV5: conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_CONV4:
+      case L_DCONV6: conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, lds, b0, nb); break;
+      case L_CONV8: conv_mfma_body<64, 32, 5, 2, false, 4, 8, 1, 1, 4, IN_F32, OUT_U8_LATENT, false>(a, lds, b0, nb); break;
+      case L_DCONV1: conv_mfma_body<32, 64, 5, 2, true, 8, 8, 2, 2, 1, IN_U8_LATENT, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_DCONV7: conv_mfma_body<64, 64, 5, 2, true, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      default: break;
+    }
+  }
+}
+
+static void conv_tiles(LayerId id, ConvArgs& a) {  // launch_conv's tile grid for layer id
+  const bool tr = id == L_DCONV1 || id == L_DCONV7;
+  int th = 8, tw = 16;
+  if (id == L_CONV2 || id == L_DCONV1) tw = 8;
+  if (id == L_CONV8) th = 4, tw = 8;
+  const int gy = tr ? a.H : a.OH, gx = tr ? a.W : a.OW;
+  a.tiles_y = (gy + th - 1) / th;
+  a.tiles_x = (gx + tw - 1) / tw;
+}
+
+hipError_t chain_add_layer(Fp32Chain& ch, LayerId id, ConvArgs a) {
+  if (ch.nstage >= kChainMax || id == L_CONV1 || id == L_DCONV8 || id >= L_COUNT) return hipErrorInvalidValue;
+  conv_tiles(id, a);
+  if ((long long)a.tiles_y * a.tiles_x * a.P > INT32_MAX) return hipErrorInvalidValue;
+  ch.kind[ch.nstage] = id;
+  ch.c[ch.nstage++] = a;
+  return hipSuccess;
+}
+
+hipError_t chain_add_conv1(Fp32Chain& ch, Conv1Args a) {
+  if (ch.nstage >= kChainMax) return hipErrorInvalidValue;
+  a.tiles_y = (a.OH + C1_T - 1) / C1_T;
+  a.tiles_x = (a.OW + C1_T - 1) / C1_T;
+  ch.kind[ch.nstage++] = L_CONV1;
+  ch.c1 = a;
+  return hipSuccess;
+}
+
+hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a) {
+  if (ch.nstage >= kChainMax) return hipErrorInvalidValue;
+  a.tiles_y = (a.H + D8_TH - 1) / D8_TH;
+  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
+  ch.kind[ch.nstage++] = L_DCONV8;
+  ch.d8 = a;
+  return hipSuccess;
+}
+
+hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st) {
+  if (ch.nstage == 0) return hipSuccess;
+  if (!ch.bar || !ch.gate.gate) return hipErrorInvalidValue;
+  Fp32Chain arg = ch;
+  void* args[] = {&arg};
+  return hipLaunchCooperativeKernel((const void*)fp32_chain_kernel, dim3(device_cus()), dim3(256), args, 0, st);
+}
+
 static int fp32_grid(const RangeGuard& rg, long long jobs) {
   static const int gated_per_cu = [] {
     const char* e = std::getenv("NIC_GATE_GRID");
     return e ? std::max(1, std::atoi(e)) : 1;
   }();
+  static const int gated_blocks = [] {  // A/B: absolute block count of the gated grids
+    const char* e = std::getenv("NIC_GATE_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  if (rg.gate && gated_blocks) return (int)std::min<long long>(jobs, gated_blocks);
   return (int)std::min<long long>(jobs, (long long)(rg.gate ? gated_per_cu : 8) * device_cus());
 }
 
