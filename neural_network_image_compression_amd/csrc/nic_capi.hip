@@ -337,7 +337,10 @@ EncGeom enc_geom(int n, int h, int w) {
   g.c8y = same_pad(g.c2y.out, 5, 2);
   g.c8x = same_pad(g.c2x.out, 5, 2);
   const size_t P = 3 * (size_t)n;
-  g.r0 = P * g.c1y.out * g.c1x.out * 32;
+  // R0: conv1's output, or (conv1 fused into conv2) the padded split colour planes
+  int oy, ox, hp, wp;
+  c12_plane_geom(g.c2y.out, g.c2x.out, g.c2y.lo, g.c2x.lo, g.c1y.lo, g.c1x.lo, &oy, &ox, &hp, &wp);
+  g.r0 = std::max(P * g.c1y.out * g.c1x.out * 32, (2 * P * (size_t)hp * wp + 1) / 2);
   g.r123 = P * g.c2y.out * g.c2x.out * 64;
   return g;
 }
@@ -730,6 +733,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
     a2.W0 = w;
     a2.p1y = g.c1y.lo;
     a2.p1x = g.c1x.lo;
+    a2.cplane = (uint16_t*)R[0];  // colour planes (R0 is free: conv1 writes no output)
     TIMED(L_CONV2, launch_conv12_x3(a2, st));
   } else {
     TIMED(L_CONV2, run(L_CONV2, a2));

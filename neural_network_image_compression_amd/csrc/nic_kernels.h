@@ -61,6 +61,8 @@ struct ConvArgs {
   const float* bias1;     // [2][32]
   int H0, W0;             // image size (conv1 input)
   int p1y, p1x;           // conv1 TF-SAME pad_lo
+  uint16_t* cplane;       // padded split colour planes [hi, lo][P][cp_h][cp_w] f16 (c12_plane_geom)
+  int cp_h, cp_w;
   // dconv8 projection fused into dconv7 (f16x3): per dconv7 output pixel the 25 phase-tap
   // dot products with dconv8's kernel, tile-major [P][4 phases][tiles_y][tiles_x][25][64 px]
   float* proj;
@@ -116,6 +118,9 @@ hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const f
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA
 hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st);  // conv1 fused into conv2 (f16x3)
+// the fused conv1's padded colour planes: origin offsets and plane size in f16 elements
+// (a.cplane must hold 2 * P * hp * wp of them)
+void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int* oy, int* ox, int* hp, int* wp);
 bool conv12_fused();  // whether nic_encode uses launch_conv12_x3 in f16x3 mode
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);      // exact fp32 VALU

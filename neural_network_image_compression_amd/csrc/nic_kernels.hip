@@ -1130,6 +1130,19 @@ struct HaloDma {
   }
 };
 
+// fl(h + l) for the f16 halves `S` of dwords H and L: one v_fma_mix_f32 (l * 1 + h, exact
+// product and sum, one rounding) instead of two conversions and an add -- bit-identical to
+// __fadd_rn((float)h, (float)l)
+template <int S>
+__device__ __forceinline__ float add_f16_pair(unsigned H, unsigned L) {
+  float t;
+  if constexpr (S == 0)
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(L), "v"(H));
+  else
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(t) : "v"(L), "v"(H));
+  return t;
+}
+
 // ------------------------------------------------------------------------------------
 // Weight-stationary persistent conv (split-f16 on v_mfma_f32_16x16x32_f16) over a
 // stride-1 window of KH x KW taps: the k3 s1 layers (KH = KW = 3), and each of the four
@@ -1376,8 +1389,12 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         if constexpr (RESID) {
           f16x4 rh, rl;
           unswap16(rq[m], rh, rl);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = __fadd_rn(v[r], __fadd_rn((float)rh[r], (float)rl[r]));
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 H = __builtin_bit_cast(u32x2, rh), L = __builtin_bit_cast(u32x2, rl);
+          static_for<4>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            v[r] = __fadd_rn(v[r], add_f16_pair<r & 1>(H[r >> 1], L[r >> 1]));
+          });
         }
         if (y < a.H && x < a.W) range_track(rmax, v);
         f16x4 hi, lo;
@@ -1856,25 +1873,75 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 
 // conv1 + conv2 fused and software-pipelined (split-f16; encoder.py:10-11, 20-21 with the
 // colour front end utils.py:74-77), the tap-split weight-stationary form of ws2_wave with
-// two conv2 halo buffers so that conv1 of tile i+1 runs beside conv2 of tile i:
-//   [B_top] ts 0: epilogue of tile i-1 (own sums + the ts 1 partials) | ts 1: colour patch
-//   of tile i+1 from RGB bytes loaded one tile earlier
-//   [B1] ts 0: conv1 share of tile i+1 -> conv2 stream of tile i | ts 1: RGB loads of tile
-//   i+2, conv2 stream of tile i, its partial sums, conv1 share of tile i+1.
-// Two barriers per tile (the unpipelined form needs three, and its conv1 phase ran on all
-// 8 waves at once with the matrix pipes idle); SIMD partners (w, w + 4) are the two tap
-// halves of one channel group and meet the conv1 VALU work of one with the conv2 MFMA
-// stream of the other.  conv1 of tile k writes halo buffer k & 1; the patch and the partial
-// tile are single buffers (each barrier orders their reuse).  LDS: 2 x 57 KB + 16 + 9.5 KB.
-// u8 x -> fp32(x) / 255 correctly rounded without the LUT: q = x * fp32(1/255), then one
-// FMA residual correction (exact for all 256 bytes; same values as c_u8_to_unit)
-#ifndef NIC_C12_LUT
-#define NIC_C12_LUT 0
+// two conv2 halo buffers so that conv1 of tile i+1 runs beside conv2 of tile i.
+//
+// The colour planes come from a pre-pass (colour_split_kernel): every RGB pixel's Y, Cb, Cr
+// (x/255, ((r k0 + g k1) + b k2) + off, every op rounded) split once into f16 hi / lo
+// planes with a zero border wide enough for every tile's 41 x 42 patch (conv1's SAME
+// padding), so a tile's patch is a plain LDS-DMA of 2 x 41 rows and conv1 reads its
+// im2col B fragments (tap pairs = 2 consecutive f16) straight from LDS with no split.
+// (Computing the patch per tile from the RGB bytes -- each colour value 6.6 times over,
+// plus the split per im2col element -- made the kernel VALU-issue bound.)
+//
+// One block barrier per tile.  After B_top(i): halo i, patch i+1 and the partials of
+// tile i-1 are complete.
+//   ts 0: epilogue(i-1) (own sums + the ts 1 partials) -> flag -> its conv1(i+1) share ->
+//         conv2 stream of tile i
+//   ts 1: patch DMA of tile i+2 -> conv2 stream of tile i -> (flag: partials(i-1) read) ->
+//         partials(i) -> its conv1(i+1) share -> vmcnt(0)
+// The partials pass only between the two waves of one channel group (SIMD partners w and
+// w + 4), so an LDS flag orders them instead of a second block barrier.  conv1 of tile k
+// writes halo buffer k & 1 and reads patch buffer k & 1.
+// LDS: 2 halos (2 x 57 KB) + partials 16 KB + 2 patches (2 x 7 KB).
+constexpr int C12_PPW = 21;                          // patch row pitch in dwords (42 f16 columns)
+constexpr int C12_PPIECE = (C12_PH * C12_PPW + 63) / 64;  // 1-dword-per-lane DMA pieces per plane (14)
+constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in LDS (hi or lo)
+#ifndef NIC_C12_PT0
+#define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
-__device__ __forceinline__ float u8_unit(unsigned x) {
-  const float xf = (float)x, r = 0.0039215688593685627f;  // fp32(1/255)
-  const float q = __fmul_rn(xf, r);
-  return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, xf), r, q);
+
+// Padded colour planes of the fused conv1 (ConvArgs::cplane): origin offsets and sizes in
+// f16 elements for conv2's tile grid, so that tile (ty, tx)'s patch starts at row 32 ty,
+// column 32 tx (dword aligned) and every patch element lies inside the plane.
+void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int* oy, int* ox, int* hp, int* wp) {
+  const int ty = (OH + 7) / 8, tx = (OW + 7) / 8;
+  *oy = 2 * pad_y + p1y;
+  *ox = 2 * pad_x + p1x;
+  *hp = 32 * (ty - 1) + C12_PH;
+  *wp = 32 * (tx - 1) + 2 * C12_PPW;
+}
+
+// One thread per (image, padded row, column pair): the three colour planes of two pixels,
+// split into hi / lo f16 (zero outside the image), one dword store per plane and half.
+__global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __restrict__ rgb, uint16_t* __restrict__ cp,
+                                                           int N, int H, int W, int oy, int ox, int hp, int wp) {
+  const int pairs = wp / 2;
+  const long long total = (long long)N * hp * pairs;
+  const size_t plane = (size_t)hp * wp, P = 3 * (size_t)N;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int c2 = (int)(t % pairs);
+    const long long r = t / pairs;
+    const int yp = (int)(r % hp), n = (int)(r / hp);
+    const int y = yp - oy;
+    float v[3][2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int x = 2 * c2 + e - ox;
+      const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const uint8_t* px = rgb + (((size_t)n * H + (in ? y : 0)) * W + (in ? x : 0)) * 3;
+      const float r8 = c_u8_to_unit[px[0]], g8 = c_u8_to_unit[px[1]], b8 = c_u8_to_unit[px[2]];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v[k][e] = in ? __fadd_rn(project(c_ycbcr + 3 * k, r8, g8, b8), c_ycbcr_off[k]) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const _Float16 h0 = (_Float16)v[k][0], h1 = (_Float16)v[k][1];
+      const _Float16 l0 = (_Float16)(v[k][0] - (float)h0), l1 = (_Float16)(v[k][1] - (float)h1);
+      const size_t o = ((size_t)k * N + n) * plane + (size_t)yp * wp + 2 * c2;  // plane k N + n
+      *(uint32_t*)(cp + o) = (uint32_t)__builtin_bit_cast(uint16_t, h0) | (uint32_t)__builtin_bit_cast(uint16_t, h1) << 16;
+      *(uint32_t*)(cp + P * plane + o) = (uint32_t)__builtin_bit_cast(uint16_t, l0) | (uint32_t)__builtin_bit_cast(uint16_t, l1) << 16;
+    }
+  }
 }
 
 template <int TS>
@@ -1884,9 +1951,9 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   using G = GeomS2<CIN, TH, TW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
   constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
-  char* part = lds + 2 * G::HALO_BYTES;         // [NCG] partial tiles of the ts = 1 waves
-  float* plane = (float*)(part + NCG * PART);   // colour-plane patch
-  float* lut = plane + C12_PH * C12_PP;         // u8 -> fp32 / 255
+  char* part = lds + 2 * G::HALO_BYTES;           // [NCG] partial tiles of the ts = 1 waves
+  char* patches = part + NCG * PART;              // [2 parities][hi, lo] patch planes
+  int* pflag = (int*)(patches + 4 * C12_PLANE);   // [NCG] last tile whose partials ts 0 has read
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -1923,7 +1990,9 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     t0x = (r - ty * a.tiles_x) * TW;
   };
 
-  // conv1 A fragments / bias / scale and this lane's im2col tap offsets (-1: pad tap >= 25)
+  // conv1 A fragments / bias / scale and this lane's im2col tap-pair offsets in a patch
+  // plane (bytes; pair = kh * 3 + kw / 2; pad pairs >= 15 read any finite element: their
+  // weights are zero)
   f16x8 A1[2][2];
   f32x4 b1[2];
   {
@@ -1936,131 +2005,103 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     }
   }
   const float scale1 = a.wscale1[model];
-  int toff[4];  // patch offsets of this lane's 4 tap pairs (k = 2 * pair + e: pair = kh * 3 + kw / 2)
+  int poff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int pr = 4 * g + j;
-    toff[j] = pr < 15 ? (pr / 3) * C12_PP + 2 * (pr % 3) : -1;
+    poff[j] = pr < 15 ? ((pr / 3) * C12_PPW + pr % 3) * 4 : 0;
   }
-  constexpr int NRGB = (C12_PH * C12_PH + 255) / 256;  // patch pixels per ts = 1 thread
-  uint32_t rgb_b[NRGB][2];  // raw bytes of this thread's patch pixels (ts = 1 waves): r | g << 8, b
-  uint32_t rgb_in = 0;      // bit j: pixel j lies inside the image
-  int pl_type = 0;          // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
-  const int tid1 = (int)threadIdx.x - 256;
-  // per thread and patch pixel j (idx = tid1 + 256 j): its byte offset from the patch origin
-  // in the image and its (row, column) packed r | c << 8 (0xffff: no pixel)
-  unsigned pix_off[NRGB], pix_rc[NRGB];
+  // ts 1: the patch DMA of a tile, 2 planes x C12_PPIECE pieces over the 4 ts 1 waves;
+  // per lane and piece the byte offset from the patch origin in a colour plane
+  constexpr int NPD = (2 * C12_PPIECE + 3) / 4;  // pieces per ts 1 wave (7)
+  unsigned doff[NPD];
   if constexpr (TS == 1) {
 #pragma unroll
-    for (int j = 0; j < NRGB; ++j) {
-      const int idx = tid1 + 256 * j;
-      const int r = idx / C12_PH, c = idx - r * C12_PH;
-      const bool ok = idx < C12_PH * C12_PH;
-      pix_off[j] = ok ? (unsigned)((r * a.W0 + c) * 3) : 0u;
-      pix_rc[j] = ok ? (unsigned)(r | c << 8) : 0xffffu;
+    for (int j = 0; j < NPD; ++j) {
+      const int k = cg + 4 * j, q = (k % C12_PPIECE) * 64 + lane;
+      const int row = q / C12_PPW, dc = q - row * C12_PPW;
+      doff[j] = k < 2 * C12_PPIECE && q < C12_PH * C12_PPW ? (unsigned)((row * a.cp_w + 2 * dc) * 2) : kDmaOOR;
     }
   }
-  // RGB bytes of tile i's patch: buffer loads over image n (rows above / below the image
-  // read zeros; the inside mask zeroes the rest), plain registers consumed by the next phase A
-  auto rgb_load = [&](int i) {
+  const size_t cp_plane = (size_t)a.cp_h * a.cp_w;  // f16 elements per colour plane
+  auto patch_dma = [&](int i) {  // tile i's patch into patch buffer i & 1
     int p, t0y, t0x;
     tile_at(i, p, t0y, t0x);
-    const int n = p % a.nimg;
-    pl_type = p / a.nimg;
-    const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
-    const unsigned img_bytes = (unsigned)(a.H0 * a.W0 * 3);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.rgb + (size_t)n * img_bytes), (short)0, (int)img_bytes, kBufWord3);
-    const unsigned org = (unsigned)((py0 * a.W0 + px0) * 3);
-    rgb_in = 0;
+    const unsigned org = (unsigned)((4 * t0y * a.cp_w + 4 * t0x) * 2);
+    char* dst = patches + (i & 1) * 2 * C12_PLANE;
 #pragma unroll
-    for (int j = 0; j < NRGB; ++j) {
-      const int r = (int)(pix_rc[j] & 255), c = (int)(pix_rc[j] >> 8);
-      const bool inside = pix_rc[j] != 0xffffu && (unsigned)(py0 + r) < (unsigned)a.H0 && (unsigned)(px0 + c) < (unsigned)a.W0;
-      const unsigned v = inside ? pix_off[j] + org : kDmaOOR;
-      rgb_b[j][0] = __builtin_amdgcn_raw_buffer_load_b16(rs, (int)v, 0, 0);      // r, g
-      rgb_b[j][1] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(v + 2u), 0, 0);  // b
-      rgb_in |= (inside ? 1u : 0u) << j;
-    }
-  };
-  // colour plane of the patch (utils.py:74-77: x/255, ((r k0 + g k1) + b k2) + off, every op
-  // rounded), zero outside the image (conv1's SAME padding)
-  auto patch = [&]() {
-    const float* kk = c_ycbcr + pl_type * 3;
-    const float off = c_ycbcr_off[pl_type];
-#pragma unroll
-    for (int j = 0; j < NRGB; ++j) {
-      if (pix_rc[j] != 0xffffu) {
-        const int r = (int)(pix_rc[j] & 255), c = (int)(pix_rc[j] >> 8);
-#if NIC_C12_LUT
-        const float r8 = lut[rgb_b[j][0] & 255], g8 = lut[rgb_b[j][0] >> 8], b8 = lut[rgb_b[j][1]];
-#else
-        const float r8 = u8_unit(rgb_b[j][0] & 255), g8 = u8_unit(rgb_b[j][0] >> 8), b8 = u8_unit(rgb_b[j][1]);
-#endif
-        plane[r * C12_PP + c] = ((rgb_in >> j) & 1) ? __fadd_rn(project(kk, r8, g8, b8), off) : 0.f;
-      }
+    for (int j = 0; j < NPD; ++j) {
+      const int k = cg + 4 * j;  // wave-uniform
+      if (k >= 2 * C12_PPIECE) break;
+      const int hl = k / C12_PPIECE;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.cplane + ((size_t)hl * a.P + p) * cp_plane), (short)0, (int)(cp_plane * 2), kBufWord3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + hl * C12_PLANE + (k % C12_PPIECE) * 256), 4,
+                                               (int)(doff[j] == kDmaOOR ? kDmaOOR : doff[j] + org), 0, 0, 0);
     }
   };
   float rmax = 0.f;  // range guard of the split outputs (conv2's, and conv1's into the halo)
-  // conv1 of tile i on the 19 x 19 halo pixels into halo buffer i & 1: px-tiles of 16, two
-  // 16-channel tiles each, three px-tiles per wave software-pipelined
+  // this role's share of conv1 of tile i on the 19 x 19 halo pixels (patch buffer i & 1 ->
+  // halo buffer i & 1): pixel tiles PTB + cg + 4u, two 16-channel tiles each, software-
+  // pipelined (all fragment reads, then the MFMA chains, then the epilogues)
   auto conv1 = [&](int i) {
-    int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
-    char* halo = lds + (i & 1) * G::HALO_BYTES;
-    const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;  // halo origin, conv1-output coords
-    constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + NW - 1) / NW;
-    f32x2 xv[PTW][4];
+    constexpr int NPT = (G::HH * G::HW + 15) / 16, PT0 = NIC_C12_PT0, PT1 = (NPT - 4 * PT0 + 3) / 4;
+    static_assert(PT0 >= 0 && PT1 >= 0 && 4 * (PT0 + PT1) >= NPT, "conv1 shares cover the halo");
+    constexpr int PTW = TS == 0 ? PT0 : PT1, PTB = TS == 0 ? 0 : 4 * PT0;
+    if constexpr (PTW > 0) {
+      int p, t0y, t0x;
+      tile_at(i, p, t0y, t0x);
+      char* halo = lds + (i & 1) * G::HALO_BYTES;
+      const char* ph = patches + (i & 1) * 2 * C12_PLANE;
+      const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;  // halo origin, conv1-output coords
+      f16x8 bh[PTW], bl[PTW];
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-      const int q = 16 * (wave + NW * u) + l16;
-      const int qq = q < G::HH * G::HW ? q : 0;
-      const int hy = qq / G::HW, hx = qq - hy * G::HW;
-      const float* pb = plane + 2 * hy * C12_PP + 2 * hx;
+      for (int u = 0; u < PTW; ++u) {
+        const int q = 16 * (PTB + cg + 4 * u) + l16;
+        const int qq = q < G::HH * G::HW ? q : 0;
+        const int hy = qq / G::HW, hx = qq - hy * G::HW;
+        const char* pb = ph + (2 * hy * C12_PPW + hx) * 4;
+        u32x4 H, L;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xv[u][j] = toff[j] >= 0 ? *(const f32x2*)(pb + toff[j]) : (f32x2){0.f, 0.f};
-    }
-    f16x8 bh[PTW], bl[PTW];
-#pragma unroll
-    for (int u = 0; u < PTW; ++u)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = xv[u][j >> 1][j & 1];
-        const _Float16 hh = (_Float16)x;
-        bh[u][j] = hh;
-        bl[u][j] = (_Float16)(x - (float)hh);
+        for (int j = 0; j < 4; ++j) {
+          H[j] = *(const uint32_t*)(pb + poff[j]);
+          L[j] = *(const uint32_t*)(pb + C12_PLANE + poff[j]);
+        }
+        bh[u] = __builtin_bit_cast(f16x8, H);
+        bl[u] = __builtin_bit_cast(f16x8, L);
       }
-    f32x4 c1[PTW][2];
+      f32x4 c1[PTW][2];
 #pragma unroll
-    for (int u = 0; u < PTW; ++u)
+      for (int u = 0; u < PTW; ++u)
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl[u], c1[u][ct], 0, 0, 0);
-        c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh[u], c1[u][ct], 0, 0, 0);
-      }
+        for (int ct = 0; ct < 2; ++ct) {
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl[u], c1[u][ct], 0, 0, 0);
+          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh[u], c1[u][ct], 0, 0, 0);
+        }
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-      const int pt = wave + NW * u;
-      if (pt >= NPT) break;  // wave-uniform
-      const int q = 16 * pt + l16;
-      const bool qv = q < G::HH * G::HW;
-      const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
-      const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
+      for (int u = 0; u < PTW; ++u) {
+        const int pt = PTB + cg + 4 * u;
+        if (pt >= NPT) break;  // wave-uniform
+        const int q = 16 * pt + l16;
+        const bool qv = q < G::HH * G::HW;
+        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
+        const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        f32x4 v;
+        for (int ct = 0; ct < 2; ++ct) {
+          f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
-        range_track(rmax, v);
-        f16x4 hi, lo;
-        split4(v, hi, lo);
-        // swap16_pair: even-g lanes hold the hi of channels 16 ct + 4 g .. +7, odd-g lanes
-        // the lo of the same 8: one 16-B store per lane (2-way bank conflicts with the
-        // 160-B records) instead of two 8-B stores (4-way)
-        const u32x4 q16 = swap16_pair(hi, lo);
-        if (qv)
-          *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * ct + 4 * (g & ~1)) * 2) = q16;
+          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
+          range_track(rmax, v);
+          f16x4 hi, lo;
+          split4(v, hi, lo);
+          // swap16_pair: even-g lanes hold the hi of channels 16 ct + 4 g .. +7, odd-g lanes
+          // the lo of the same 8: one 16-B store per lane (2-way bank conflicts with the
+          // 160-B records) instead of two 8-B stores (4-way)
+          const u32x4 q16 = swap16_pair(hi, lo);
+          if (qv)
+            *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * ct + 4 * (g & ~1)) * 2) = q16;
+        }
       }
     }
   };
@@ -2125,18 +2166,15 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     }
   };
 
-  // prologue: patch 0 -> conv1 0 (halo 0)
-  if constexpr (TS == 1)
-    if (ntile > 0) rgb_load(0);
-  for (int q = threadIdx.x; q < 256; q += 64 * NW) lut[q] = c_u8_to_unit[q];
-  for (int q = threadIdx.x; q < C12_PH * C12_PP; q += 64 * NW) plane[q] = 0.f;  // pad columns
-  __syncthreads();  // LUT and zeroed pads before any patch store
+  // prologue: patches 0 and 1, conv1 of tile 0
+  if (threadIdx.x < NCG) pflag[threadIdx.x] = 0;
   if constexpr (TS == 1) {
-    if (ntile > 0) patch();
-    if (ntile > 1) rgb_load(1);
+    if (ntile > 0) patch_dma(0);
+    if (ntile > 1) patch_dma(1);
+    dma_wait_all();
   }
   lds_reads_done();
-  stage_barrier();  // patch 0 complete
+  stage_barrier();  // patches 0, 1 complete
   if (ntile > 0) conv1(0);
 #ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
   unsigned long long sx[8] = {}, sa, sb;
@@ -2153,36 +2191,47 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   do {               \
   } while (0)
 #endif
+  // One block barrier per tile.  After B_top(i): halo i, patch i+1 and the partials of
+  // tile i-1 are complete.
+  //   ts 0: epilogue(i-1) (reads the partials) -> flag -> its conv1(i+1) share -> stream(i)
+  //   ts 1: RGB loads of tile i+2 -> stream(i) -> (flag: partials(i-1) read) -> partials(i)
+  //         -> its conv1(i+1) share -> patch(i+2) into the buffer conv1(i) read
+  // The partials pass between the two waves of one channel group only (SIMD partners), so
+  // an LDS flag orders them instead of a second block barrier.
   for (int i = 0; i <= ntile; ++i) {
     C12_MARK(6);
     lds_reads_done();
-    stage_barrier();  // B_top: halo i complete, partials of tile i-1 written, the patch free
+    stage_barrier();  // B_top
     C12_MARK(0);
     if constexpr (TS == 0) {
-      if (i > 0) epilogue(i - 1);
-    } else {
-      if (i + 1 < ntile) patch();  // tile i+1, from the RGB bytes loaded during tile i-1's phase B
-    }
-    C12_MARK(1);
-    if (i == ntile) break;
-    lds_reads_done();
-    stage_barrier();  // B1: patch of tile i+1 complete; the partial tiles read
-    C12_MARK(2);
-    if constexpr (TS == 0) {
+      if (i > 0) {
+        epilogue(i - 1);
+        lds_reads_done();  // the partial reads have returned
+        __hip_atomic_store(pflag + cg, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      C12_MARK(1);
+      if (i == ntile) break;
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
       stream(i);
       C12_MARK(5);
     } else {
-      if (i + 2 < ntile) rgb_load(i + 2);  // in flight during the stream
+      if (i == ntile) break;
+      if (i + 2 < ntile) patch_dma(i + 2);  // into the buffer conv1(i) read; lands during the stream
       C12_MARK(4);
       stream(i);
+      C12_MARK(5);
+      if (i > 0)
+        while (__hip_atomic_load(pflag + cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < i)
+          __builtin_amdgcn_s_sleep(1);
+      C12_MARK(2);
       char* pp = part + cg * PART + lane * 16;
 #pragma unroll
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
-      C12_MARK(5);
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
+      dma_wait_all();  // patch i+2 landed (before B_top(i+1) publishes it)
+      C12_MARK(1);
     }
   }
 #ifdef NIC_STAMPS
@@ -2203,7 +2252,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
 
 __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
   using G = GeomS2<32, 8, 8>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + (C12_PH * C12_PP + 256) * 4];
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -3420,9 +3469,22 @@ static bool c12_serial() {
   return on;
 }
 
-hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st) {
+hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
   if (!a.rgb || !a.wx1 || !a.bias1 || a.H0 <= 0 || a.W0 <= 0) return hipErrorInvalidValue;
   if (c12_serial()) return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
+  if (!a.cplane || a.OH <= 0 || a.OW <= 0) return hipErrorInvalidValue;
+  int oy, ox;
+  c12_plane_geom(a.OH, a.OW, a.pad_y, a.pad_x, a.p1y, a.p1x, &oy, &ox, &a.cp_h, &a.cp_w);
+  // 32-bit byte offsets inside one plane (buffer resources of the patch DMA)
+  if ((long long)a.cp_h * a.cp_w * 2 >= (1LL << 31)) return hipErrorInvalidValue;
+  const long long work = (long long)a.nimg * a.cp_h * (a.cp_w / 2);
+  if (work == 0) return hipSuccess;
+  const int blocks = (int)std::min<long long>((work + 255) / 256, 16LL * device_cus());
+  hipLaunchKernelGGL(colour_split_kernel, dim3(blocks), dim3(256), 0, st, a.rgb, a.cplane, a.nimg, a.H0, a.W0, oy, ox,
+                     a.cp_h, a.cp_w);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
 }
 

@@ -74,6 +74,9 @@ int main() {
   a.H0 = H0;
   a.W0 = W0;
   a.p1y = a.p1x = 1;
+  int oy, ox, hp, wp;  // padded split colour planes of the fused conv1
+  c12_plane_geom(OH, OW, a.pad_y, a.pad_x, a.p1y, a.p1x, &oy, &ox, &hp, &wp);
+  CK(hipMalloc(&a.cplane, (size_t)2 * P * hp * wp * 2));
   const int maxb = 1024;
   unsigned long long* st;
   CK(hipMalloc(&st, (size_t)maxb * 64 * 8));
@@ -95,7 +98,7 @@ int main() {
   ms /= iters;
   std::vector<unsigned long long> hs((size_t)maxb * 64);
   CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
-  const char* nm[7] = {"top-bar", "epi/patch", "B1-bar", "conv1", "rgb-issue", "stream", "other"};
+  const char* nm[7] = {"top-bar", "epi|patch", "flag-wait", "(part+)conv1", "rgb-issue", "stream", "other"};
   printf("conv12 %.4f ms (%.0f TFLOP/s)\n", ms, 85.564 / ms);
 #ifdef NIC_STAMPS
   for (int w = 0; w < 8; w += 4) {

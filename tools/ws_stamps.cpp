@@ -99,14 +99,13 @@ int main() {
     std::vector<unsigned long long> hs(maxb * 8);
     CK(hipMemcpy(hs.data(), st, maxb * 64, hipMemcpyDeviceToHost));
     // per tap-set group: sums
-    double w[26] = {}, eo[26] = {}, ep[26] = {}, mf[26] = {}, nt[26] = {}, life[26] = {}, rt[26] = {}, nb[26] = {};
+    double w[26] = {}, ep[26] = {}, mf[26] = {}, nt[26] = {}, life[26] = {}, rt[26] = {}, nb[26] = {};
     int nblk = 0;
     for (int b = 0; b < maxb; ++b) {
       if (hs[b * 8 + 5] == 0) continue;
       ++nblk;
       const int k = (int)hs[b * 8 + 6];
       w[k] += hs[b * 8 + 0];
-      eo[k] += hs[b * 8 + 7];
       ep[k] += hs[b * 8 + 1];
       mf[k] += hs[b * 8 + 2];
       nt[k] += hs[b * 8 + 3];
@@ -119,9 +118,9 @@ int main() {
       if (nb[k] == 0) continue;
       const double per = nt[k];
       printf("  taps %2d: %4.0f blocks, tiles/block %5.1f, clock %.2f GHz, life %8.0f cyc; per tile: wait %5.0f  "
-             "epi %5.0f + issue %5.0f  mfma %5.0f (ideal %5.0f = 2 waves x %d MFMA x 16)\n",
+             "epi+issue %5.0f  mfma %5.0f (ideal %5.0f = 2 waves x %d MFMA x 16)\n",
              k, nb[k], per / nb[k], 0.1 * life[k] / rt[k],
-             life[k] / nb[k], w[k] / per, eo[k] / per, (ep[k] - eo[k]) / per, mf[k] / per, 2.0 * k * 2 * 4 * 3 * 16, k * 2 * 4 * 3);
+             life[k] / nb[k], w[k] / per, ep[k] / per, mf[k] / per, 2.0 * k * 2 * 4 * 3 * 16, k * 2 * 4 * 3);
     }
     CK(hipFree(in));
     CK(hipFree(out));
