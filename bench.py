@@ -182,6 +182,7 @@ def power_probe(device, weights, x, z, r, dom, flop, steps, peak):
     lt = c.layer_times()
     c.set_timing(False)
     torch.cuda.synchronize()
+    c.close()  # release the second context now (not from a finaliser at interpreter exit)
     ms, n = lt[dom]
     avg = ms / max(n, 1)
     tf = flop / (avg * 1e-3) / 1e12
@@ -377,6 +378,8 @@ def main():
                       ("" if args.workload == "4k" else " and recons") + ", once after the timed steps"}
     if rank != 0:
         barrier()
+        torch.cuda.synchronize()
+        codec.close()
         if world > 1:
             dist.destroy_process_group()
         return
@@ -472,6 +475,8 @@ def main():
         out["roofline"]["power_probe"] = power_probe(local, weights, x, z, r, dom, flops[dom], args.steps, peak)
     print(json.dumps(out), flush=True)
     barrier()
+    torch.cuda.synchronize()
+    codec.close()
     if world > 1:
         dist.destroy_process_group()
 

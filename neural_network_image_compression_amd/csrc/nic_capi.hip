@@ -680,7 +680,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   a1.OW = g.c1x.out;
   a1.pad_y = g.c1y.lo;
   a1.pad_x = g.c1x.lo;
-  // the gated exact-fp32 re-run: all layers recorded into one cooperative launch
+  // the gated exact-fp32 re-run: all layers recorded into one launch (fp32_chain_kernel)
   Fp32Chain chain{};
   const bool chained = !x3 && rg.gate && use_chain();
   chain.gate = rg;
@@ -766,7 +766,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   // the re-run's head is dconv1 (it counts the trip); later layers only gate
   RangeGuard rgl = rg;
   rgl.trips = nullptr;
-  Fp32Chain chain{};  // the gated exact-fp32 re-run as one cooperative launch (see encode_pass)
+  Fp32Chain chain{};  // the gated exact-fp32 re-run as one launch (see encode_pass)
   const bool chained = !x3 && rg.gate && use_chain();
   chain.gate = rg;
   chain.bar = c->range + 2;

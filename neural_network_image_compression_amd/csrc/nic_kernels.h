@@ -97,7 +97,7 @@ struct Dconv8Args {
   int tiles_y7, tiles_x7;      // gather kernel: dconv7's 8x8 tile grid over its coarse input
 };
 
-// The gated exact-fp32 re-run of a split-f16 pass as one cooperative launch (stages run in
+// The gated exact-fp32 re-run of a split-f16 pass as one launch (stages run in
 // order with grid barriers; every block exits at once unless gate.gate == gate.epoch).
 constexpr int kChainMax = 6;
 struct Fp32Chain {

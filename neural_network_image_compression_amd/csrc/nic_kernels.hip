@@ -3160,8 +3160,8 @@ __global__ __launch_bounds__(256) void unpack_latent_kernel(const uint8_t* __res
 // (conv1 / conv_mfma layers / dconv8) in sequence, a grid barrier between stages.  When
 // the split pass stayed in range every block exits at the gate, so the pass costs one
 // dispatch instead of one per layer (each dispatch, even of an empty kernel, holds the
-// queue for ~5 us: measured 4.7-5.3 us for 1 to 256 blocks).  Cooperative launch, one
-// block per CU (all resident, as the barrier needs).
+// queue for ~5 us: measured 4.7-5.3 us for 1 to 256 blocks).  One block per CU (all
+// resident, as the barrier needs).
 // ------------------------------------------------------------------------------------
 template <class... Gs>
 constexpr int max_lds_floats() {
@@ -3258,9 +3258,12 @@ hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a) {
 hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st) {
   if (ch.nstage == 0) return hipSuccess;
   if (!ch.bar || !ch.gate.gate) return hipErrorInvalidValue;
-  Fp32Chain arg = ch;
-  void* args[] = {&arg};
-  return hipLaunchCooperativeKernel((const void*)fp32_chain_kernel, dim3(device_cus()), dim3(256), args, 0, st);
+  // one 256-thread block per CU (the kernel's LDS and VGPRs allow one per CU), so every
+  // block of the grid barrier can be resident; a plain launch: blocks held back by another
+  // stream's kernel start as soon as it frees its CU (nothing it waits on depends on this
+  // kernel).  (hipLaunchCooperativeKernel made the process crash at exit under rocprofv3.)
+  hipLaunchKernelGGL(fp32_chain_kernel, dim3(device_cus()), dim3(256), 0, st, ch);
+  return hipGetLastError();
 }
 
 static int fp32_grid(const RangeGuard& rg, long long jobs) {
