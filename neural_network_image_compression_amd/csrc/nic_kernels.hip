@@ -1216,6 +1216,11 @@ struct GeomWS {
 // sum_ci h[px][ci] w8[tap][ci] on the same split-f16 MFMA (2 tap blocks x 2 k32-steps x 3,
 // B fragments from an LDS copy of w8), scaled by 2^-k8 and stored tile-major (a.proj).
 // One extra barrier per tile (hproj complete); the next tile's barrier orders its reuse.
+// residual of the k3 layers: LDS-DMA per wave (NIC_RES_DMA=1, default) or VGPR loads
+#ifndef NIC_RES_DMA
+#define NIC_RES_DMA 1
+#endif
+constexpr bool kResDma = NIC_RES_DMA != 0;
 // diagnostic build only: no projection MFMAs / stores in dconv7 (wrong results)
 #ifdef NIC_DIAG_NOPROJ
 constexpr bool kProjOff = true;
@@ -1235,7 +1240,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   // (same-box A/B: with HaloDma its stream carries ~8x the s_waitcnt instructions -- exact
   // lgkmcnt counts instead of lgkmcnt(0) drains -- which the residual epilogue's partner
   // wave cannot absorb), while HaloDma saves 2-3 % on conv3 / dconv5 / dconv7
-  constexpr bool kBufHalo = !RESID;
+  constexpr bool kBufHalo = !RESID || kResDma;
   using HP = std::conditional_t<kBufHalo, HaloDma<G, CIN, NW>, HaloPieces<G, CIN, CIN, NW>>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
 
@@ -1314,6 +1319,9 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 
   f32x4 acc[MT];
   u32x4 rq[MT];  // split residual of the tile in flight (RESID), in the 16-B store layout
+  // kResDma: the residual tile DMA'd into this wave's LDS region (MT pieces of 1 KB, lane l
+  // at 16 l: the granule it reads back) instead of into VGPRs
+  char* res_lds = lds + 2 * G::HALO_BYTES + wave * MT * 1024;
   // 16-B output granule of this lane after swap16_pair: [hi | lo] half (g & 1), channels
   // 16w + 8 (g >> 1) .. +7
   const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
@@ -1388,6 +1396,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
         if constexpr (RESID) {
           f16x4 rh, rl;
+          if constexpr (kResDma) rq[m] = *(const u32x4*)(res_lds + m * 1024 + lane * 16);
           unswap16(rq[m], rh, rl);
           typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
           const u32x2 H = __builtin_bit_cast(u32x2, rh), L = __builtin_bit_cast(u32x2, rl);
@@ -1439,7 +1448,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int oy = min(ep_y + 2 * m + (l16 >> 3), a.OH - 1), ox = min(ep_x + (l16 & 7), a.OW - 1);
-        rq[m] = *(const u32x4*)(a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off);
+        const uint16_t* src = a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off;
+        if constexpr (kResDma)
+          dma16((const char*)src, res_lds + m * 1024);  // this wave's own region: its reads came first
+        else
+          rq[m] = *(const u32x4*)src;
       }
     }
     const char* buf = lds + (i & 1) * G::HALO_BYTES;
@@ -2286,7 +2299,8 @@ template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = f
 __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
   using G = GeomWS<CIN, TH, TW>;
   __shared__ __attribute__((aligned(16)))
-  char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 + TH * TW * COUT * 4 : 0)];
+  char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 + TH * TW * COUT * 4 : 0) +
+           (RESID && kResDma ? (COUT / 16) * (TH * TW / 16) * 1024 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];

@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int layer = 0; layer < 2; ++layer) {
+  for (int layer = 0; layer < 3; ++layer) {
     ConvArgs a{};
     a.in_s = in;
     a.zero16 = zero16;
@@ -95,9 +95,12 @@ int main(int argc, char** argv) {
       a.OH = H;
       a.OW = W;
       a.out_s = out;
+      a.res_s = in;  // conv4: residual of the same shape
       gflop = 57.982;
     }
-    auto go = [&] { return layer == 0 ? launch_dconv7_proj_x3(a, 0) : launch_layer_x3(L_CONV3, a, 0); };
+    auto go = [&] {
+      return layer == 0 ? launch_dconv7_proj_x3(a, 0) : launch_layer_x3(layer == 1 ? L_CONV3 : L_CONV4, a, 0);
+    };
     for (int it = 0; it < 30; ++it) CK(go());
     CK(hipEventRecord(e0, 0));
     for (int it = 0; it < iters; ++it) CK(go());
@@ -106,7 +109,8 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
-    printf("%-7s %.4f ms  %.1f TFLOP/s  frac %.3f\n", layer == 0 ? "dconv7" : "conv3", ms, gflop / ms, gflop / ms / 833.3);
+    printf("%-7s %.4f ms  %.1f TFLOP/s  frac %.3f\n", layer == 0 ? "dconv7" : layer == 1 ? "conv3" : "conv4", ms,
+           gflop / ms, gflop / ms / 833.3);
 #ifdef NIC_STAMPS
     std::vector<unsigned long long> hs(maxb * 8);
     CK(hipMemcpy(hs.data(), st, maxb * 64, hipMemcpyDeviceToHost));
