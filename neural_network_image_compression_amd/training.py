@@ -293,16 +293,21 @@ class Training:
         W.save_tf(w, os.path.join(self.checkpoint_dir, "decoder"), "decoder")
 
     def __call__(self, x: np.ndarray, x_val_path: Optional[str], max_epochs: int, batch_size: int,
-                 entropy_loss_coef: float, verbose: bool = True) -> List[Dict[str, object]]:
-        """training.py:53-165: epochs over shuffled batches of the u8 array x (N,H,W,3)."""
+                 entropy_loss_coef: float, verbose: bool = True,
+                 epoch_samples: Optional[int] = None) -> List[Dict[str, object]]:
+        """training.py:53-165: epochs over shuffled batches of the u8 array x (N,H,W,3).
+        ``epoch_samples``: the epoch length in images when x is a subset of the reference's
+        training set (each epoch then walks that many images over reshuffled passes of x, so
+        the per-epoch coefficient schedule keeps the reference's pace); None = one pass."""
         torch = _torch()
         rng = np.random.default_rng(self.seed)
         log = []
         step = 0
+        per_epoch = epoch_samples or len(x)
         for epoch in range(self.epoch, max_epochs):
             self.epoch = epoch
-            order = rng.permutation(len(x))
-            for i in range(0, len(x), batch_size):
+            order = np.concatenate([rng.permutation(len(x)) for _ in range(-(-per_epoch // len(x)))])[:per_epoch]
+            for i in range(0, per_epoch, batch_size):
                 m = self.train_step(torch.from_numpy(np.ascontiguousarray(x[order[i:i + batch_size]])),
                                     entropy_loss_coef)
                 m["epoch"] = epoch

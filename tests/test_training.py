@@ -61,6 +61,16 @@ def test_train_step_cpu(tmp_path):
         np.testing.assert_array_equal(v, after[k])
 
 
+def test_epoch_samples_cpu(tmp_path):
+    """An epoch of `epoch_samples` images over reshuffled passes of a smaller subset (the
+    reference's epoch length over its full set); the coefficient schedule steps per epoch."""
+    tr = T.Training(device="cpu", seed=0, checkpoint_dir=str(tmp_path) + "/")
+    log = tr(_smooth(3, 32, 32, 4), None, max_epochs=2, batch_size=2, entropy_loss_coef=0.01, verbose=False,
+             epoch_samples=5)
+    assert len(log) == 6  # ceil(5 / 2) steps per epoch
+    assert [m["epoch"] for m in log] == [0, 0, 0, 1, 1, 1]
+
+
 @pytest.mark.gpu
 def test_trained_weights_into_hip_codec(tmp_path):
     """GPU training steps -> TF checkpoint (training.py:167-172) -> Encoder.load -> HIP encode

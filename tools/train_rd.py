@@ -1,13 +1,17 @@
 """Config-4 RD sweep with trained models: train the codec (training.py, the reference's
-loss) at entropy_loss_coef 0.01 / 0.02 / 0.03 (training.py:54), then evaluate each trained
-set with the device RD harness (rd.py) whole-image and as 256^2 tiles.
+Training with its loss, optimisers and per-epoch coefficient schedule) from each initial
+entropy_loss_coef (SURVEY config 4: 0.01 / 0.02 / 0.03; the reference's main uses 0.01,
+tf2_0/src/training.py:179), then evaluate each trained set with the device RD harness
+(rd.py) on the reference's Kodak image kodim21 (768x512), whole-image and as 256^2 tiles.
 
-Data: no dataset travels to the GPU box, so training uses synthetic smooth 128^2 patches
-and the evaluation synthetic smooth 512x768 images (Kodak size).  Short runs: the curve
-shows the harness end to end, not the reference's converged RD numbers.
+Data: the reference's own training patches, a 1,000-patch subset committed under
+data/imagenet_patches_1k (tools/make_train_subset.py); an epoch is --epoch-samples images
+(default 19,000 = the reference's epoch over all of data/imagenet_patches) drawn from
+reshuffled passes of the subset, so the coefficient schedule keeps the reference's pace.
 
-    python tools/train_rd.py [steps]
+    python tools/train_rd.py [--epochs 10] [--batch 64] [--steps N] [--out FILE]
 """
+import argparse
 import json
 import os
 import sys
@@ -24,45 +28,64 @@ from neural_network_image_compression_amd import weights as W  # noqa: E402
 from neural_network_image_compression_amd.rd import rd_sweep  # noqa: E402
 
 
-def smooth_images(n, h, w, seed):
-    rng = np.random.default_rng(seed)
-    a = np.cumsum(np.cumsum(rng.integers(-2, 3, (n, h, w, 3)), axis=1), axis=2).astype(np.float64)
-    a -= a.min(axis=(1, 2, 3), keepdims=True)
-    a *= 255.0 / np.maximum(a.max(axis=(1, 2, 3), keepdims=True), 1)
-    return a.astype(np.uint8)
+def load_patches(d):
+    from PIL import Image
+    names = sorted(f for f in os.listdir(d) if f.endswith(".jpg"))
+    return np.stack([np.asarray(Image.open(os.path.join(d, f)).convert("RGB")) for f in names])
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-    batch = 16
-    x = smooth_images(batch * 8, 128, 128, 0)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data", default=os.path.join(ROOT, "data", "imagenet_patches_1k"))
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--epoch-samples", type=int, default=19000)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=0, help="stop each run after this many steps (0: all epochs)")
+    ap.add_argument("--coefs", default="0.01,0.02,0.03")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    x = load_patches(args.data)
+    with np.load(os.path.join(ROOT, "tests", "golden", "kodim21_full.npz"), allow_pickle=False) as g:
+        ev = g["x"]  # the reference's data/kodak_img/kodim21.png, (1, 512, 768, 3)
     sets, train_log = {}, {}
-    for coef in (0.01, 0.02, 0.03):
+    for coef in (float(c) for c in args.coefs.split(",")):
         t0 = time.perf_counter()
         with tempfile.TemporaryDirectory() as d:
-            tr = T.Training(device="cuda", weights=W.seeded_weights(0), seed=0, checkpoint_dir=d + "/")
-            log = []
-            epochs = max(1, -(-steps * batch // len(x)))
-            log = tr(x, None, max_epochs=epochs, batch_size=batch, entropy_loss_coef=coef, verbose=False)[:steps]
+            tr = T.Training(device="cuda", weights=W.seeded_weights(0, init="glorot"), seed=0, checkpoint_dir=d + "/")
+            epochs = args.epochs
+            if args.steps:
+                epochs = min(epochs, -(-args.steps * args.batch // args.epoch_samples))
+            t1 = time.perf_counter()
+            log = tr(x, None, max_epochs=epochs, batch_size=args.batch, entropy_loss_coef=coef, verbose=True,
+                     epoch_samples=args.epoch_samples)
+            t_train = time.perf_counter() - t1
+            if args.steps:
+                log = log[:args.steps]
             tr._save()
             w = W.load(os.path.join(d, "encoder"), "encoder")
             w.update(W.load(os.path.join(d, "decoder"), "decoder"))
         label = f"coef{coef:.2f}"
         sets[label] = w
-        train_log[label] = {"steps": len(log), "seconds": round(time.perf_counter() - t0, 2),
+        tail = log[-20:]
+        train_log[label] = {"steps": len(log), "epochs": epochs, "seconds": round(time.perf_counter() - t0, 1),
+                            "train_seconds": round(t_train, 1),
                             "first": {k: log[0][k] for k in ("ssim", "bpp", "entropy_loss")},
-                            "last": {k: log[-1][k] for k in ("ssim", "bpp", "entropy_loss")}}
+                            "last20_mean": {k: [float(np.mean([m[k][j] for m in tail])) for j in range(3)]
+                                            for k in ("ssim", "bpp")}}
         print(label, json.dumps(train_log[label]), flush=True)
-    ev = smooth_images(4, 512, 768, 1)
     res = rd_sweep(sets, ev, tile=256)
-    out = {"config": "config4: trained at entropy_loss_coef 0.01/0.02/0.03 (short runs on synthetic 128^2 "
-                     "patches), evaluated on 4 synthetic 512x768 images, whole and 256^2 tiles",
+    out = {"config": f"config4: trained from entropy_loss_coef {args.coefs} (+0.01 per epoch, training.py:165), "
+                     f"{args.epochs} epochs of {args.epoch_samples} images, batch {args.batch}, on the reference's "
+                     "ImageNet patches (1,000-patch subset); evaluated on kodim21 768x512, whole and 256^2 tiles",
            "train": train_log, "points": {}}
     for label, modes in res.items():
         out["points"][label] = {mode: {k: (round(v, 6) if isinstance(v, float) else v) for k, v in d.items()
                                        if k.endswith("_mean") or k in ("tile", "tile_border_psnr_delta_db")}
                                 for mode, d in modes.items()}
     print(json.dumps(out), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
