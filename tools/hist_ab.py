@@ -36,3 +36,21 @@ for v in ["1", "4", "8", "8z"]:
     ok = ref is None or bool(torch.equal(cn, ref))
     ref = cn if ref is None else ref
     print(f"NIC_HIST={v:3s} {ms * 1e3:7.1f} us  {z.numel() / (ms * 1e-3) / 1e9:7.1f} GB/s  counts_equal={ok}", flush=True)
+# latent value distribution (how skewed the bins are: same-address LDS atomics serialise)
+cn = ref.double()
+for pl in range(3):
+    p = cn[pl] / cn[pl].sum()
+    top = torch.topk(p, 4)
+    print(f"plane {pl}: top bins {top.indices.tolist()} share {[round(v, 3) for v in top.values.tolist()]}")
+# streaming reference: a torch int32 sum over the same bytes
+zi = z.view(-1).view(torch.int32)
+for _ in range(3):
+    zi.sum()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(20):
+    zi.sum()
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / 20
+print(f"torch int32 sum: {ms * 1e3:7.1f} us  {z.numel() / (ms * 1e-3) / 1e9:7.1f} GB/s")
