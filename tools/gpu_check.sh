@@ -31,7 +31,7 @@ fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o kt \
-    -- python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --no-parity --no-power-probe > "$OUT/${TAG}_prof.log" 2>&1
+    -- python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --no-parity --no-power-probe --no-host-path --no-quality > "$OUT/${TAG}_prof.log" 2>&1
   rc=$?; tail -3 "$OUT/${TAG}_prof.log"; stop_on $rc rocprof
   find "$OUT/${TAG}_prof" -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-220
 fi

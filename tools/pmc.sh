@@ -7,7 +7,7 @@ OUT="$ROOT/gpurun_out"
 TAG="${1:-pmc}"
 mkdir -p "$OUT/${TAG}_pmc"
 export TMPDIR=/tmp
-BENCH=(python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity)
+BENCH=(python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-power-probe --no-host-path --no-quality)
 if [ "${LIST:-0}" = 1 ]; then
   timeout -k 10 120 rocprofv3 -L > "$OUT/${TAG}_pmc/counters.txt" 2>&1
   echo "[list] rc=$?"
