@@ -1959,7 +1959,7 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
 
 template <int TS>
 __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
-  constexpr int CIN = 32, COUT = 64, NTS = 2, TH = 8, TW = 8, MT = 4, NCG = 4, KST = 1, NW = 8;
+  constexpr int CIN = 32, COUT = 64, NTS = 2, TH = 8, TW = 8, MT = 4, NCG = 4, KST = 1;
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
