@@ -410,6 +410,7 @@ def main():
             flops[name] = 0
             layers[name] = {"avg_ms": round(avg, 4), "gbytes_per_launch": round(nbytes / 1e9, 3),
                             "gbps": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None,
+                            "hbm_frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if avg > 0 else None,
                             "fused": "gather of dconv7's tap projections + inverse colour + quantiser"}
             continue
         extra = moved.get(name)

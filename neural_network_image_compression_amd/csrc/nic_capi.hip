@@ -1144,6 +1144,56 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
   return NIC_OK;
 }
 
+// ---- training side path (nic_train.hip) ----------------------------------------------------
+static bool train_dims_ok(int c) { return c >= 1 && c <= 64; }
+
+int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
+                    int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales, float* y,
+                    int oh, int ow, int cout, void* stream) {
+  if (n < 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
+      !train_dims_ok(cin) || !train_dims_ok(cout) || pad_y < 0 || pad_x < 0)
+    return fail(NIC_ESHAPE, "nic_conv_gather: bad shape n=%d %dx%dx%d -> %dx%dx%d k=%dx%d s=%d pad=%d,%d", n, h, w, cin,
+                oh, ow, cout, kh, kw, stride, pad_y, pad_x);
+  if ((wt_layout != 0 && wt_layout != 1) || (transposed != 0 && transposed != 1))
+    return fail(NIC_EINVAL, "nic_conv_gather: wt_layout / transposed must be 0 or 1");
+  if (n == 0) return NIC_OK;
+  if (!x || !wt || !y) return fail(NIC_EINVAL, "nic_conv_gather: NULL argument");
+  HIP_TRY(launch_conv_gather(x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed, bias, scales, y,
+                             oh, ow, cout, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_conv_wgrad_work(int n, int uh, int uw, int kh, int kw, int ca, int cb, int64_t* floats) {
+  if (!floats) return fail(NIC_EINVAL, "nic_conv_wgrad_work: NULL argument");
+  if (n < 0 || uh <= 0 || uw <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || !train_dims_ok(ca) || !train_dims_ok(cb))
+    return fail(NIC_ESHAPE, "nic_conv_wgrad_work: bad shape");
+  *floats = (int64_t)train_wgrad_work_floats(n, uh, uw, kh, kw, ca, cb);
+  return NIC_OK;
+}
+
+int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb, int kh,
+                   int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw, float* work,
+                   int64_t work_floats, void* stream) {
+  if (n < 0 || gh <= 0 || gw <= 0 || uh <= 0 || uw <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
+      !train_dims_ok(ca) || !train_dims_ok(cb) || pad_y < 0 || pad_x < 0)
+    return fail(NIC_ESHAPE, "nic_conv_wgrad: bad shape");
+  if (!dw) return fail(NIC_EINVAL, "nic_conv_wgrad: NULL argument");
+  const int64_t need = (int64_t)train_wgrad_work_floats(n, uh, uw, kh, kw, ca, cb);
+  if (n > 0 && (!gat || !dir || !work)) return fail(NIC_EINVAL, "nic_conv_wgrad: NULL argument");
+  if (n > 0 && work_floats < need)
+    return fail(NIC_EINVAL, "nic_conv_wgrad: work holds %lld floats, needs %lld", (long long)work_floats, (long long)need);
+  HIP_TRY(launch_conv_wgrad(gat, n, gh, gw, ca, dir, uh, uw, cb, kh, kw, stride, pad_y, pad_x, scales, dw, work,
+                            (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_absmax_scale(const float* x, int64_t count, float* scale, float* work, void* stream) {
+  if (count < 0) return fail(NIC_ESHAPE, "nic_absmax_scale: negative count");
+  if (!scale || !work || (count > 0 && !x)) return fail(NIC_EINVAL, "nic_absmax_scale: NULL argument");
+  HIP_TRY(launch_absmax_scale(x, count, scale, work, (hipStream_t)stream));
+  return NIC_OK;
+}
+
 int nic_set_precision(nic_ctx* c, int mode) {
   if (!c) return fail(NIC_EINVAL, "nic_set_precision: NULL ctx");
   if (mode != NIC_PRECISION_FP32 && mode != NIC_PRECISION_F16X3)

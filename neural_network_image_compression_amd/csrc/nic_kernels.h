@@ -173,4 +173,15 @@ hipError_t launch_ms_ssim(const uint8_t* a, const uint8_t* b, int nimg, int H, i
 hipError_t launch_sq_err(const uint8_t* a, const uint8_t* b, int nimg, int64_t bytes, unsigned long long* sse,
                          hipStream_t st);
 
+// --- training side path (nic_train.hip) ------------------------------------------------------
+size_t train_scale_work_floats();
+size_t train_wgrad_work_floats(int n, int uh, int uw, int kh, int kw, int ca, int cb);
+hipError_t launch_absmax_scale(const float* x, long long n, float* scale, float* work, hipStream_t st);
+hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int layout,
+                              int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales,
+                              float* y, int oh, int ow, int cout, hipStream_t st);
+hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb,
+                             int kh, int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw,
+                             float* work, hipStream_t st);
+
 }  // namespace nic

@@ -6,6 +6,10 @@ restated so that trained weights exist for the codec and the config-4 RD sweep:
 * ``Entropynet`` (training.py:25-42): conv 64 k5 s2 -> conv 64 k3 -> conv 64 k3 ->
   Flatten (NHWC order, as Keras) -> Dense 512 -> Dense 1 -> clip [0, 8], a learned bpp
   estimate of one latent plane.
+* Convolutions (``backend="hip"``, the default): every conv of the step -- encoder,
+  decoder, Entropynet; forward, input and kernel gradients -- runs on the HIP split-f16x3
+  MFMA kernels of ``csrc/nic_train.hip`` (``train_hip``), NHWC; ``backend="torch"`` keeps
+  the PyTorch-autograd restatement (MIOpen) the HIP path is tested against.
 * ``Training.__call__`` (training.py:53-165): per batch, /255, random left-right and
   up-down flips per image, RGB -> YCbCr planes, the Y model on Y and the CbCr model on
   Cb||Cr, uniform noise U(-0.5, 0.5)/255 on the latent as the quantisation proxy, the PNG
@@ -71,25 +75,36 @@ def tconv_same(x, kernel_hwoi, bias, stride: int):
     return F.leaky_relu(y, 0.2)
 
 
-def base_encoder(p: Dict[str, object], x):
-    """encoder.py:7-32 on NCHW planes (N,1,H,W) -> (N,32,h,w)."""
-    x = conv_same(x, p["conv1/kernel"], p["conv1/bias"], 2)
-    x = conv_same(x, p["conv2/kernel"], p["conv2/bias"], 2)
+def _convs(hip: bool):
+    if hip:
+        from . import train_hip
+
+        return train_hip.conv_same, train_hip.tconv_same
+    return conv_same, tconv_same
+
+
+def base_encoder(p: Dict[str, object], x, hip: bool = False):
+    """encoder.py:7-32 on planes (N,1,H,W) NCHW -> (N,32,h,w), or with ``hip`` on NHWC
+    (N,H,W,1) -> (N,h,w,32) through the HIP training convolutions (train_hip)."""
+    conv, _ = _convs(hip)
+    x = conv(x, p["conv1/kernel"], p["conv1/bias"], 2)
+    x = conv(x, p["conv2/kernel"], p["conv2/bias"], 2)
     res = x
-    x = conv_same(x, p["conv3/kernel"], p["conv3/bias"], 1)
-    x = conv_same(x, p["conv4/kernel"], p["conv4/bias"], 1)
-    x = conv_same(x + res, p["conv8/kernel"], p["conv8/bias"], 2)
+    x = conv(x, p["conv3/kernel"], p["conv3/bias"], 1)
+    x = conv(x, p["conv4/kernel"], p["conv4/bias"], 1)
+    x = conv(x + res, p["conv8/kernel"], p["conv8/bias"], 2)
     return x.clamp(0, 1)
 
 
-def base_decoder(p: Dict[str, object], x):
-    """decoder.py:7-32 on NCHW latents (N,32,h,w) -> (N,1,8h,8w)."""
-    x = tconv_same(x, p["dconv1/kernel"], p["dconv1/bias"], 2)
+def base_decoder(p: Dict[str, object], x, hip: bool = False):
+    """decoder.py:7-32 on latents (N,32,h,w) NCHW -> (N,1,8h,8w), or NHWC with ``hip``."""
+    _, tconv = _convs(hip)
+    x = tconv(x, p["dconv1/kernel"], p["dconv1/bias"], 2)
     res = x
-    x = tconv_same(x, p["dconv5/kernel"], p["dconv5/bias"], 1)
-    x = tconv_same(x, p["dconv6/kernel"], p["dconv6/bias"], 1)
-    x = tconv_same(x + res, p["dconv7/kernel"], p["dconv7/bias"], 2)
-    x = tconv_same(x, p["dconv8/kernel"], p["dconv8/bias"], 2)
+    x = tconv(x, p["dconv5/kernel"], p["dconv5/bias"], 1)
+    x = tconv(x, p["dconv6/kernel"], p["dconv6/bias"], 1)
+    x = tconv(x + res, p["dconv7/kernel"], p["dconv7/bias"], 2)
+    x = tconv(x, p["dconv8/kernel"], p["dconv8/bias"], 2)
     return x.clamp(0, 1)
 
 
@@ -106,9 +121,10 @@ def _gauss_window(torch, device, dtype, size: int = 11, sigma: float = 1.5):
     return g.to(device=device, dtype=dtype)
 
 
-def ssim(x, y, max_val: float = 1.0):
+def ssim(x, y, max_val: float = 1.0, hip: bool = False):
     """tf.image.ssim (11x11 Gaussian sigma 1.5, k1 0.01, k2 0.03, VALID) of NCHW planes ->
-    (N,) mean over the valid map and channels; differentiable."""
+    (N,) mean over the valid map and channels; differentiable.  ``hip``: the Gaussian runs on
+    the HIP gather GEMM (one-channel planes)."""
     torch = _torch()
     import torch.nn.functional as F
 
@@ -116,6 +132,10 @@ def ssim(x, y, max_val: float = 1.0):
     c = x.shape[1]
 
     def filt(t):
+        if hip:
+            from . import train_hip
+
+            return train_hip.gauss_valid(t, g)
         t = F.conv2d(t, g.view(1, 1, 1, -1).expand(c, 1, 1, -1), groups=c)
         return F.conv2d(t, g.view(1, 1, -1, 1).expand(c, 1, -1, 1), groups=c)
 
@@ -163,12 +183,14 @@ class Entropynet:
     def parameters(self) -> List[object]:
         return list(self.p.values())
 
-    def __call__(self, z):
+    def __call__(self, z, hip: bool = False):
+        """z: (M,32,h,w) NCHW, or (M,h,w,32) NHWC with ``hip`` (HIP convolutions)."""
         p = self.p
-        x = conv_same(z, p["conv1/kernel"], p["conv1/bias"], 2)
-        x = conv_same(x, p["conv2/kernel"], p["conv2/bias"], 1)
-        x = conv_same(x, p["conv3/kernel"], p["conv3/bias"], 1)
-        x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # Keras Flatten of NHWC
+        conv, _ = _convs(hip)
+        x = conv(z, p["conv1/kernel"], p["conv1/bias"], 2)
+        x = conv(x, p["conv2/kernel"], p["conv2/bias"], 1)
+        x = conv(x, p["conv3/kernel"], p["conv3/bias"], 1)
+        x = (x if hip else x.permute(0, 2, 3, 1)).reshape(x.shape[0], -1)  # Keras Flatten of NHWC
         x = x @ p["dense1/kernel"] + p["dense1/bias"]
         x = x @ p["dense2/kernel"] + p["dense2/bias"]
         return x.clamp(0, 8)
@@ -198,8 +220,16 @@ class Training:
     the target's byte counts may differ from TF's by the two zlib front ends."""
 
     def __init__(self, device: str = "cuda", weights: Optional[W.Weights] = None, seed: int = 0,
-                 checkpoint_dir: str = "../checkpoints/"):
+                 checkpoint_dir: str = "../checkpoints/", backend: Optional[str] = None):
+        """backend "hip" (default on a GPU): every convolution of the step, forward and
+        backward, on the HIP split-f16x3 MFMA kernels (train_hip, NHWC); "torch" (default on
+        the CPU): PyTorch autograd convolutions (MIOpen / oneDNN, NCHW) -- the restatement the
+        HIP path is tested against."""
         torch = _torch()
+        backend = backend or ("hip" if torch.device(device).type == "cuda" else "torch")
+        if backend not in ("hip", "torch"):
+            raise ValueError(f"backend must be 'hip' or 'torch', not {backend!r}")
+        self.hip = backend == "hip"
         self.device = torch.device(device)
         w = weights if weights is not None else W.seeded_weights(seed, init="glorot")  # Keras defaults
         self.params = {k: torch.tensor(np.asarray(v, np.float32), device=self.device, requires_grad=True)
@@ -232,37 +262,8 @@ class Training:
     def train_step(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
         """One batch (training.py:67-147): u8 NHWC images (B,H,W,3) -> metrics."""
         torch = _torch()
-        x = images.to(self.device)
-        b = x.shape[0]
-        self._setup(x.shape[1:3])
-        img = x.float() / 255
-        if flip:  # random_flip_left_right / random_flip_up_down, per image
-            lr = torch.rand(b, generator=self._gen, device=self.device) < 0.5
-            ud = torch.rand(b, generator=self._gen, device=self.device) < 0.5
-            img = torch.where(lr.view(-1, 1, 1, 1), img.flip(2), img)
-            img = torch.where(ud.view(-1, 1, 1, 1), img.flip(1), img)
-        planes = colour_planes(img)
-        p0, p1 = planes[0], torch.cat(planes[1:], dim=0)
-        enc0 = base_encoder(self._model("encoderY"), p0)
-        enc1 = base_encoder(self._model("encoderCbCr"), p1)
-        noise = lambda t: torch.rand(t.shape, generator=self._gen, device=self.device) - 0.5  # noqa: E731
-        noisy0 = (enc0 + noise(enc0) / 255).clamp(0, 1)
-        noisy1 = (enc1 + noise(enc1) / 255).clamp(0, 1)
-        batch_enc = torch.cat([enc0, enc1], dim=0)
-        aprox = self.entropy_model(batch_enc)  # (3B, 1)
-        codes = torch.round(batch_enc.detach() * 255).clamp(0, 255).to(torch.uint8)
-        bpp = png_bpp_planes(codes.permute(0, 2, 3, 1).contiguous().cpu().numpy(), float(x.shape[1] * x.shape[2]),
-                             self._pool)
-        bpp_t = torch.from_numpy(bpp).to(self.device).view(-1, 1)
-        aprox_entropy_loss = ((bpp_t - aprox) ** 2).mean()
-        ent = torch.split(aprox, b, dim=0)
-        dec0 = base_decoder(self._model("decoderY"), noisy0)
-        dec1 = base_decoder(self._model("decoderCbCr"), noisy1)
-        ssim0 = ssim(p0, dec0).mean()
-        ssim1_each = ssim(p1, dec1)
-        ssim1 = ssim1_each.mean()
-        loss0 = ((1 - ssim0) / 2 + entropy_loss_coef * ent[0]).sum()
-        loss1 = ((1 - ssim1) / 2 + 0.01 * torch.cat(ent[1:], dim=0)).sum()  # reference: 0.01 (training.py:124)
+        f = self.losses(images, entropy_loss_coef, flip)
+        loss0, loss1, aprox_entropy_loss = f["loss0"], f["loss1"], f["entropy_loss"]
         opt_y, opt_c, opt_e = self._opt
         ent_params = self.entropy_model.parameters()
         # three tapes: main losses update the codec models only, the entropy loss the net only
@@ -278,10 +279,60 @@ class Training:
                 group["eps"] = keras_adam_eps(int(st) + 1)
             opt.step()
             opt.zero_grad(set_to_none=True)
-        cb, cr = torch.split(ssim1_each.detach(), b)
-        return {"ssim": [float(ssim0.detach()), float(cb.mean()), float(cr.mean())],
+        b = images.shape[0]
+        cb, cr = torch.split(f["ssim1_each"].detach(), b)
+        bpp = f["bpp"]
+        return {"ssim": [float(f["ssim0"].detach()), float(cb.mean()), float(cr.mean())],
                 "bpp": [float(v.mean()) for v in np.split(bpp, 3)],
                 "entropy_loss": float(aprox_entropy_loss.detach()), "loss": [float(loss0.detach()), float(loss1.detach())]}
+
+    def losses(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
+        """The step's forward pass (training.py:67-126): the two codec losses, the entropy
+        net's loss and the tensors the metrics read (differentiable w.r.t. the parameters)."""
+        torch = _torch()
+        x = images.to(self.device)
+        b = x.shape[0]
+        self._setup(x.shape[1:3])
+        img = x.float() / 255
+        if flip:  # random_flip_left_right / random_flip_up_down, per image
+            lr = torch.rand(b, generator=self._gen, device=self.device) < 0.5
+            ud = torch.rand(b, generator=self._gen, device=self.device) < 0.5
+            img = torch.where(lr.view(-1, 1, 1, 1), img.flip(2), img)
+            img = torch.where(ud.view(-1, 1, 1, 1), img.flip(1), img)
+        planes = colour_planes(img)
+        p0, p1 = planes[0], torch.cat(planes[1:], dim=0)
+        hip = self.hip
+        if hip:  # one channel: (N,1,H,W) and (N,H,W,1) share their memory layout
+            p0, p1 = p0.reshape(p0.shape[0], *p0.shape[2:], 1), p1.reshape(p1.shape[0], *p1.shape[2:], 1)
+        enc0 = base_encoder(self._model("encoderY"), p0, hip)
+        enc1 = base_encoder(self._model("encoderCbCr"), p1, hip)
+
+        def noise(t):  # drawn in NCHW order in both layouts (same stream of numbers)
+            shape = (t.shape[0], t.shape[3], t.shape[1], t.shape[2]) if hip else t.shape
+            u = torch.rand(shape, generator=self._gen, device=self.device) - 0.5
+            return u.permute(0, 2, 3, 1) if hip else u
+
+        noisy0 = (enc0 + noise(enc0) / 255).clamp(0, 1)
+        noisy1 = (enc1 + noise(enc1) / 255).clamp(0, 1)
+        batch_enc = torch.cat([enc0, enc1], dim=0)
+        aprox = self.entropy_model(batch_enc, hip)  # (3B, 1)
+        codes = torch.round(batch_enc.detach() * 255).clamp(0, 255).to(torch.uint8)
+        codes = codes if hip else codes.permute(0, 2, 3, 1)
+        bpp = png_bpp_planes(codes.contiguous().cpu().numpy(), float(x.shape[1] * x.shape[2]), self._pool)
+        bpp_t = torch.from_numpy(bpp).to(self.device).view(-1, 1)
+        aprox_entropy_loss = ((bpp_t - aprox) ** 2).mean()
+        ent = torch.split(aprox, b, dim=0)
+        dec0 = base_decoder(self._model("decoderY"), noisy0, hip)
+        dec1 = base_decoder(self._model("decoderCbCr"), noisy1, hip)
+        if hip:  # back to (N,1,H,W) views for the SSIM filter
+            p0, p1, dec0, dec1 = (t.reshape(t.shape[0], 1, *t.shape[1:3]) for t in (p0, p1, dec0, dec1))
+        ssim0 = ssim(p0, dec0, hip=hip).mean()
+        ssim1_each = ssim(p1, dec1, hip=hip)
+        ssim1 = ssim1_each.mean()
+        loss0 = ((1 - ssim0) / 2 + entropy_loss_coef * ent[0]).sum()
+        loss1 = ((1 - ssim1) / 2 + 0.01 * torch.cat(ent[1:], dim=0)).sum()  # reference: 0.01 (training.py:124)
+        return {"loss0": loss0, "loss1": loss1, "entropy_loss": aprox_entropy_loss, "ssim0": ssim0,
+                "ssim1_each": ssim1_each, "bpp": bpp, "aprox": aprox}
 
     def weights(self) -> W.Weights:
         return {k: v.detach().float().cpu().numpy().copy() for k, v in self.params.items()}

@@ -25,6 +25,18 @@ def test_exports_every_header_symbol():
     assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with nic.h"
 
 
+def test_ctypes_signatures_match_header_arity():
+    # every declaration's parameter count equals its ctypes argtypes (a short list shifts
+    # the trailing pointers -- e.g. the stream -- into the wrong registers)
+    import re
+
+    text = re.sub(r"/\*.*?\*/", "", open(_lib.HEADER_PATH).read(), flags=re.S)
+    for name, params in re.findall(r"\b(nic_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", text):
+        params = params.strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert len(_lib._SIGNATURES[name][1]) == n, (name, n, len(_lib._SIGNATURES[name][1]))
+
+
 def test_exports_are_c_linkage():
     out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
     for s in _lib.header_symbols():

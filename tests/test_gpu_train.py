@@ -1,0 +1,150 @@
+"""HIP training convolutions (csrc/nic_train.hip via train_hip) against float64 references.
+
+Every convolution shape of the Training step (tf2_0/src/training.py:74-151): the encoder's
+Conv2Ds (encoder.py:10-17), the decoder's Conv2DTransposes (decoder.py:10-17) and the
+Entropynet's Conv2Ds (training.py:25-42) -- forward, input gradient, kernel gradient and
+bias gradient -- are compared with the torch restatement of training.py evaluated in float64
+on the CPU.  Split-f16x3 arithmetic is fp32-class: max |error| <= 2e-5 x max |reference|
+per tensor (the fp32 rounding of the float64 result alone is ~6e-8)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from neural_network_image_compression_amd import training as T  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+# (kind, cin, cout, k, stride, (h, w)) -- Keras layer shapes of the step
+SHAPES = [
+    ("conv", 1, 32, 5, 2, (34, 41)),   # conv1 (odd size: SAME pads differ per side)
+    ("conv", 32, 64, 5, 2, (17, 21)),  # conv2
+    ("conv", 64, 64, 3, 1, (12, 9)),   # conv3 / conv4 / Entropynet conv2, conv3
+    ("conv", 64, 32, 5, 2, (9, 12)),   # conv8
+    ("conv", 32, 64, 5, 2, (8, 8)),    # Entropynet conv1 on a latent
+    ("tconv", 32, 64, 5, 2, (5, 7)),   # dconv1
+    ("tconv", 64, 64, 3, 1, (10, 9)),  # dconv5 / dconv6
+    ("tconv", 64, 64, 5, 2, (9, 8)),   # dconv7
+    ("tconv", 64, 1, 5, 2, (11, 10)),  # dconv8
+]
+
+
+def _rel_err(a, ref):
+    a = a.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    return float((a - ref).abs().max() / ref.abs().max().clamp_min(1e-300))
+
+
+def _run(kind, cin, cout, k, stride, hw, n=3, gscale=1.0, seed=0):
+    from neural_network_image_compression_amd import train_hip
+
+    g = torch.Generator().manual_seed(seed)
+    h, w = hw
+    x = torch.randn((n, h, w, cin), generator=g)
+    kshape = (k, k, cin, cout) if kind == "conv" else (k, k, cout, cin)
+    kern = torch.randn(kshape, generator=g) * (1.0 / np.sqrt(k * k * cin))
+    bias = torch.randn((cout,), generator=g) * 0.1
+    # HIP, NHWC, no activation
+    xd, kd, bd = (t.cuda().requires_grad_() for t in (x, kern, bias))
+    fn = train_hip._fns()[0 if kind == "conv" else 1]
+    y = fn.apply(xd, kd, bd, stride)
+    gy = torch.randn(y.shape, generator=g) * gscale
+    y.backward(gy.cuda())
+    # float64 reference, NCHW torch restatement of training.py
+    xr, kr, br = (t.double().requires_grad_() for t in (x, kern, bias))
+    xn = xr.permute(0, 3, 1, 2)
+    if kind == "conv":
+        yr = T.conv_same(xn, kr, br, stride, act=False)
+    else:
+        import torch.nn.functional as F
+
+        # tconv_same applies leaky; undo by comparing the pre-activation: rebuild it here
+        n_out = (xn.shape[2] * stride, xn.shape[3] * stride)
+        pt, _ = T.same_pad(n_out[0], k, stride)
+        pl, _ = T.same_pad(n_out[1], k, stride)
+        full = F.conv_transpose2d(xn, kr.permute(3, 2, 0, 1), stride=stride)
+        full = F.pad(full, (0, max(0, pl + n_out[1] - full.shape[3]), 0, max(0, pt + n_out[0] - full.shape[2])))
+        yr = full[:, :, pt:pt + n_out[0], pl:pl + n_out[1]] + br.view(1, -1, 1, 1)
+    yr = yr.permute(0, 2, 3, 1)
+    yr.backward(gy.double())
+    return (y, xd.grad, kd.grad, bd.grad), (yr, xr.grad, kr.grad, br.grad)
+
+
+@pytest.mark.parametrize("kind,cin,cout,k,stride,hw", SHAPES)
+def test_conv_forward_and_gradients_match_float64(kind, cin, cout, k, stride, hw):
+    hip, ref = _run(kind, cin, cout, k, stride, hw)
+    for name, a, r in zip(("y", "dx", "dkernel", "dbias"), hip, ref):
+        assert a.shape == r.shape, name
+        assert _rel_err(a, r) <= TOL, (name, _rel_err(a, r))
+
+
+@pytest.mark.parametrize("gscale", [1e-9, 1e6])
+def test_operand_scales_keep_tiny_and_large_gradients(gscale):
+    # power-of-two operand scales: a 1e-9 gradient (below f16's smallest subnormal) and a
+    # 1e6 one (past f16's max) keep fp32-class accuracy
+    hip, ref = _run("conv", 64, 64, 3, 1, (9, 10), gscale=gscale, seed=3)
+    for name, a, r in zip(("dx", "dkernel", "dbias"), hip[1:], ref[1:]):
+        assert _rel_err(a, r) <= TOL, (name, gscale, _rel_err(a, r))
+
+
+def test_batch_of_128x128_patches_encoder_decoder_shapes():
+    # the training batch geometry (64 x 128^2 patches would be slow in float64 on the CPU;
+    # 2 patches cover every grid size of the step)
+    for kind, cin, cout, k, s, hw in [("conv", 1, 32, 5, 2, (128, 128)), ("tconv", 64, 64, 5, 2, (32, 32))]:
+        hip, ref = _run(kind, cin, cout, k, s, hw, n=2)
+        for name, a, r in zip(("y", "dx", "dkernel", "dbias"), hip, ref):
+            assert _rel_err(a, r) <= TOL, (kind, name, _rel_err(a, r))
+
+
+def test_wgrad_is_deterministic():
+    from neural_network_image_compression_amd import train_hip
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((4, 32, 32, 64), generator=g).cuda()
+    dy = torch.randn((4, 32, 32, 64), generator=g).cuda()
+    a = train_hip.wgrad(x, dy, 3, 3, 1, (1, 1))
+    b = train_hip.wgrad(x, dy, 3, 3, 1, (1, 1))
+    assert torch.equal(a, b)
+
+
+def test_hip_training_step_matches_torch_backend(tmp_path):
+    # one step's losses and parameter gradients: HIP convolutions (NHWC) vs PyTorch autograd
+    # (MIOpen, NCHW), same weights, data, flips and noise
+    from neural_network_image_compression_amd import weights as W
+
+    w0 = W.seeded_weights(0, init="glorot")
+    g = torch.Generator().manual_seed(7)
+    imgs = torch.randint(0, 256, (4, 64, 64, 3), generator=g, dtype=torch.uint8)
+    out = {}
+    for be in ("hip", "torch"):
+        tr = T.Training(device="cuda", weights=w0, seed=0, checkpoint_dir=str(tmp_path) + "/", backend=be)
+        f = tr.losses(imgs, 0.01, flip=True)
+        gy = torch.autograd.grad(f["loss0"], tr._variables("Y"), retain_graph=True)
+        gc = torch.autograd.grad(f["loss1"], tr._variables("CbCr"), retain_graph=True)
+        ge = torch.autograd.grad(f["entropy_loss"], tr.entropy_model.parameters())
+        out[be] = (f, gy, gc, ge)
+    fh, ft = out["hip"][0], out["torch"][0]
+    for key in ("loss0", "loss1", "ssim0"):
+        a, b = float(fh[key].detach()), float(ft[key].detach())
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), key
+    assert torch.allclose(fh["aprox"], ft["aprox"], rtol=1e-3, atol=1e-4)
+    for part in (1, 2):  # codec gradients (the entropy net's target may differ by a code flip)
+        for a, b in zip(out["hip"][part], out["torch"][part]):
+            assert _rel_err(a, b) <= 2e-3, _rel_err(a, b)
+
+
+def test_ssim_gaussian_on_hip_matches_float64():
+    # the SSIM loss's separable Gaussian (VALID, one channel) and its input gradient
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand((3, 1, 40, 37), generator=g)
+    y = (x + 0.05 * torch.randn(x.shape, generator=g)).clamp(0, 1)
+    xd, yd = x.cuda().requires_grad_(), y.cuda()
+    s_hip = T.ssim(xd, yd, hip=True)
+    s_hip.sum().backward()
+    xr = x.double().requires_grad_()
+    s_ref = T.ssim(xr, y.double())
+    s_ref.sum().backward()
+    assert _rel_err(s_hip, s_ref) <= TOL
+    assert _rel_err(xd.grad, xr.grad) <= 1e-4
