@@ -18,8 +18,8 @@
  *     tf2_0/tests/calc_ssim.py:13
  *   PSNR (the benchmark's quality figure)       nic_sq_err
  *   Training step convolutions, forward and     nic_conv_gather / nic_conv_wgrad /
- *     backward (tf2_0/src/training.py:74-151,     nic_absmax_scale (training side path)
- *     Keras Conv2D / Conv2DTranspose SAME)
+ *     backward (tf2_0/src/training.py:74-151,     nic_absmax_scale / nic_gauss_1d
+ *     Keras Conv2D / Conv2DTranspose SAME, SSIM)  (training side path)
  *
  * Conventions
  *  - Every buffer argument is a DEVICE pointer owned by the caller (e.g. a torch-ROCm
@@ -185,22 +185,31 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
  *                       forward; input grad of Conv2D)
  *     W(ky,kx,ci,co) = wt[((ky*kw+kx)*cin + ci)*cout + co]  (wt_layout 0, Conv2D HWIO)
  *                    = wt[((ky*kw+kx)*cout + co)*cin + ci]  (wt_layout 1, Conv2DTranspose HWOI)
- *     bias nullable; scales nullable or 2 device floats (power-of-two operand scales of x
- *     and wt from nic_absmax_scale, undone exactly in the epilogue).  cin, cout <= 64.
- * nic_conv_wgrad: dw[ky][kx][a][b] = sum over b, u of gat[b][stride*uy+ky-pad_y][stride*ux+kx-pad_x][a]
- *     * dir[b][uy][ux][b'] (Conv2D: gat = x, dir = dy, dw HWIO; Conv2DTranspose: gat = dy,
- *     dir = x, dw HWOI); deterministic (per-slice partials in `work`, summed in order).
- *     work must hold nic_conv_wgrad_work() floats.  ca, cb <= 64.
+ *     bias nullable; x_scale / w_scale nullable device floats (power-of-two operand scales from
+ *     nic_absmax_scale, undone exactly in the epilogue).  work: 16-B aligned device scratch of
+ *     nic_conv_gather_work() bytes (the split weights).  cin, cout <= 64.
+ * nic_conv_wgrad: dw[ky][kx][a][b'] = sum over b, u of
+ *     gat[b][stride*uy+ky-pad_y][stride*ux+kx-pad_x][a] * dir[b][uy][ux][b']
+ *     (Conv2D: gat = x, dir = dy, dw HWIO; Conv2DTranspose: gat = dy, dir = x, dw HWOI);
+ *     deterministic (per-slice partials in `work`, summed in order); work must hold
+ *     nic_conv_wgrad_work() floats.  ca, cb <= 64.
  * nic_absmax_scale: scale[0] = 2^(13 - floor(log2 max|x|)) (1 for 0 / non-finite), so the
- *     split-f16 operands keep every bit of tiny gradients; work >= 512 floats. */
+ *     split-f16 operands keep every bit of tiny gradients; work >= 512 floats.
+ * nic_gauss_1d: one-channel planes (n,h,w): VALID correlation with ntaps taps along x
+ *     (vertical 0) or y, or its adjoint (the input gradient); the SSIM loss's separable
+ *     Gaussian (tf.image.ssim, training.py:119-121). */
+int nic_conv_gather_work(int kh, int kw, int cin, int cout, int64_t* bytes);
 int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
-                    int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales, float* y,
-                    int oh, int ow, int cout, void* stream);
+                    int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                    const float* w_scale, float* y, int oh, int ow, int cout, void* work, int64_t work_bytes,
+                    void* stream);
 int nic_conv_wgrad_work(int n, int uh, int uw, int kh, int kw, int ca, int cb, int64_t* floats);
 int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb, int kh,
-                   int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw, float* work,
-                   int64_t work_floats, void* stream);
+                   int kw, int stride, int pad_y, int pad_x, const float* gat_scale, const float* dir_scale, float* dw,
+                   float* work, int64_t work_floats, void* stream);
 int nic_absmax_scale(const float* x, int64_t count, float* scale, float* work, void* stream);
+int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, int ntaps, int vertical, int adjoint,
+                 float* out, int h_out, int w_out, void* stream);
 
 /* Per-layer device timing.  With timing on, every kernel launch of encode/decode is
  * bracketed by a hipEvent pair on the caller's stream (the stream the kernel runs on);

@@ -1147,9 +1147,18 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
 // ---- training side path (nic_train.hip) ----------------------------------------------------
 static bool train_dims_ok(int c) { return c >= 1 && c <= 64; }
 
+int nic_conv_gather_work(int kh, int kw, int cin, int cout, int64_t* bytes) {
+  if (!bytes) return fail(NIC_EINVAL, "nic_conv_gather_work: NULL argument");
+  if (kh <= 0 || kw <= 0 || kh * kw > 64 || !train_dims_ok(cin) || !train_dims_ok(cout))
+    return fail(NIC_ESHAPE, "nic_conv_gather_work: bad shape");
+  *bytes = (int64_t)train_gather_work_bytes(kh, kw, cin, cout);
+  return NIC_OK;
+}
+
 int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
-                    int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales, float* y,
-                    int oh, int ow, int cout, void* stream) {
+                    int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                    const float* w_scale, float* y, int oh, int ow, int cout, void* work, int64_t work_bytes,
+                    void* stream) {
   if (n < 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
       !train_dims_ok(cin) || !train_dims_ok(cout) || pad_y < 0 || pad_x < 0)
     return fail(NIC_ESHAPE, "nic_conv_gather: bad shape n=%d %dx%dx%d -> %dx%dx%d k=%dx%d s=%d pad=%d,%d", n, h, w, cin,
@@ -1157,9 +1166,13 @@ int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* w
   if ((wt_layout != 0 && wt_layout != 1) || (transposed != 0 && transposed != 1))
     return fail(NIC_EINVAL, "nic_conv_gather: wt_layout / transposed must be 0 or 1");
   if (n == 0) return NIC_OK;
-  if (!x || !wt || !y) return fail(NIC_EINVAL, "nic_conv_gather: NULL argument");
-  HIP_TRY(launch_conv_gather(x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed, bias, scales, y,
-                             oh, ow, cout, (hipStream_t)stream));
+  if (!x || !wt || !y || !work) return fail(NIC_EINVAL, "nic_conv_gather: NULL argument");
+  const int64_t need = (int64_t)train_gather_work_bytes(kh, kw, cin, cout);
+  if (work_bytes < need)
+    return fail(NIC_EINVAL, "nic_conv_gather: work holds %lld bytes, needs %lld", (long long)work_bytes, (long long)need);
+  if (((uintptr_t)work & 15) != 0) return fail(NIC_EINVAL, "nic_conv_gather: work must be 16-byte aligned");
+  HIP_TRY(launch_conv_gather(x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed, bias, x_scale,
+                             w_scale, y, oh, ow, cout, work, (hipStream_t)stream));
   return NIC_OK;
 }
 
@@ -1172,8 +1185,8 @@ int nic_conv_wgrad_work(int n, int uh, int uw, int kh, int kw, int ca, int cb, i
 }
 
 int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb, int kh,
-                   int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw, float* work,
-                   int64_t work_floats, void* stream) {
+                   int kw, int stride, int pad_y, int pad_x, const float* gat_scale, const float* dir_scale, float* dw,
+                   float* work, int64_t work_floats, void* stream) {
   if (n < 0 || gh <= 0 || gw <= 0 || uh <= 0 || uw <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
       !train_dims_ok(ca) || !train_dims_ok(cb) || pad_y < 0 || pad_x < 0)
     return fail(NIC_ESHAPE, "nic_conv_wgrad: bad shape");
@@ -1182,8 +1195,23 @@ int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float*
   if (n > 0 && (!gat || !dir || !work)) return fail(NIC_EINVAL, "nic_conv_wgrad: NULL argument");
   if (n > 0 && work_floats < need)
     return fail(NIC_EINVAL, "nic_conv_wgrad: work holds %lld floats, needs %lld", (long long)work_floats, (long long)need);
-  HIP_TRY(launch_conv_wgrad(gat, n, gh, gw, ca, dir, uh, uw, cb, kh, kw, stride, pad_y, pad_x, scales, dw, work,
-                            (hipStream_t)stream));
+  HIP_TRY(launch_conv_wgrad(gat, n, gh, gw, ca, dir, uh, uw, cb, kh, kw, stride, pad_y, pad_x, gat_scale, dir_scale,
+                            dw, work, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, int ntaps, int vertical, int adjoint,
+                 float* out, int h_out, int w_out, void* stream) {
+  if (n < 0 || h_in <= 0 || w_in <= 0 || h_out <= 0 || w_out <= 0 || ntaps <= 0 || ntaps > 64)
+    return fail(NIC_ESHAPE, "nic_gauss_1d: bad shape");
+  const int d = ntaps - 1;
+  const bool ok = vertical ? (w_out == w_in && (adjoint ? h_out == h_in + d : h_out == h_in - d))
+                           : (h_out == h_in && (adjoint ? w_out == w_in + d : w_out == w_in - d));
+  if (!ok) return fail(NIC_ESHAPE, "nic_gauss_1d: output %dx%d does not match input %dx%d", h_out, w_out, h_in, w_in);
+  if (n == 0) return NIC_OK;
+  if (!in || !taps || !out) return fail(NIC_EINVAL, "nic_gauss_1d: NULL argument");
+  HIP_TRY(launch_gauss1d(in, n, h_in, w_in, taps, ntaps, vertical ? 1 : 0, adjoint ? 1 : 0, out, h_out, w_out,
+                         (hipStream_t)stream));
   return NIC_OK;
 }
 

@@ -176,12 +176,15 @@ hipError_t launch_sq_err(const uint8_t* a, const uint8_t* b, int nimg, int64_t b
 // --- training side path (nic_train.hip) ------------------------------------------------------
 size_t train_scale_work_floats();
 size_t train_wgrad_work_floats(int n, int uh, int uw, int kh, int kw, int ca, int cb);
+size_t train_gather_work_bytes(int kh, int kw, int cin, int cout);
 hipError_t launch_absmax_scale(const float* x, long long n, float* scale, float* work, hipStream_t st);
 hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int layout,
-                              int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales,
-                              float* y, int oh, int ow, int cout, hipStream_t st);
+                              int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                              const float* w_scale, float* y, int oh, int ow, int cout, void* work, hipStream_t st);
 hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb,
-                             int kh, int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw,
-                             float* work, hipStream_t st);
+                             int kh, int kw, int stride, int pad_y, int pad_x, const float* gat_scale,
+                             const float* dir_scale, float* dw, float* work, hipStream_t st);
+hipError_t launch_gauss1d(const float* in, int n, int hi, int wi, const float* taps, int nt, int vertical, int adjoint,
+                          float* out, int ho, int wo, hipStream_t st);
 
 }  // namespace nic

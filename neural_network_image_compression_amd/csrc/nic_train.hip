@@ -53,15 +53,39 @@ __device__ __forceinline__ float ld_scale(const float* s) { return s ? *s : 1.0f
 // ---- gather GEMM -------------------------------------------------------------------------
 struct GatherArgs {
   const float* x;      // [n][h][w][cin]
-  const float* wt;     // [kh*kw][cin][cout] (layout 0) or [kh*kw][cout][cin] (layout 1)
+  const f16x8* wp;     // packed split weights (pack_w_kernel): [K/32 chunk][NT/16 co tile][hi, lo][64 lanes]
   const float* bias;   // [cout] or null
   const float* sx;     // device scale of x (power of two) or null
-  const float* sw;     // device scale of wt or null
+  const float* sw;     // device scale of the weights or null (already applied in wp)
   float* y;            // [n][oh][ow][cout]
-  int n, h, w, cin, oh, ow, cout, kh, kw, stride, pad_y, pad_x, transposed, layout;
+  int n, h, w, cin, oh, ow, cout, kh, kw, stride, pad_y, pad_x, transposed;
   int K;               // kh * kw * cin
   long long M;         // n * oh * ow
+  int ph_blk[5];       // phase mode: first block of output phase (py, px) = (p >> 1, p & 1), then the grid
 };
+
+// Output pixel m of the block's set -> (b, oy, ox).  Phase mode: the pixels of one output
+// phase (oy % 2, ox % 2) = (py, px) only, so every pixel of the block uses the same taps.
+__device__ __forceinline__ bool pixel_of(const GatherArgs& a, bool ph, int py, int px, long long m, int& b, int& oy,
+                                         int& ox) {
+  if (!ph) {
+    if (m >= a.M) return false;
+    const long long per = (long long)a.oh * a.ow;
+    b = (int)(m / per);
+    const int r = (int)(m - (long long)b * per);
+    oy = r / a.ow;
+    ox = r - oy * a.ow;
+    return true;
+  }
+  const int qh = (a.oh - py + 1) >> 1, qw = (a.ow - px + 1) >> 1;
+  const long long per = (long long)qh * qw;
+  if (per == 0 || m >= (long long)a.n * per) return false;
+  b = (int)(m / per);
+  const int r = (int)(m - (long long)b * per), qy = r / qw;
+  oy = 2 * qy + py;
+  ox = 2 * (r - qy * qw) + px;
+  return true;
+}
 
 // source pixel of output pixel (b, oy, ox) at tap (ky, kx); -1 when outside / not on the grid
 __device__ __forceinline__ long long gather_src(const GatherArgs& a, int b, int oy, int ox, int ky, int kx) {
@@ -79,120 +103,168 @@ __device__ __forceinline__ long long gather_src(const GatherArgs& a, int b, int 
   return ((long long)b * a.h + iy) * a.w + ix;
 }
 
+// Weights -> split-f16 MFMA A fragments, once per call: fragment (chunk c, co tile t, hi|lo,
+// lane) holds rows co = 16 t + (lane & 15), k = 32 c + 8 (lane >> 4) + j of w * scale, where
+// k = tap * cin + ci and W(tap, ci, co) reads layout 0 [tap][ci][co] or 1 [tap][co][ci].
+__global__ __launch_bounds__(256) void pack_w_kernel(const float* __restrict__ wt, int layout, int cin, int cout, int K,
+                                                     int ntt, int nchunk, const float* __restrict__ sw,
+                                                     f16x8* __restrict__ wp) {
+  const int total = nchunk * ntt * 64;
+  const float s = ld_scale(sw);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int lane = i & 63, ct = i >> 6, t = ct % ntt, c = ct / ntt;
+    const int co = 16 * t + (lane & 15);
+    f16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * c + 8 * (lane >> 4) + j;
+      float v = 0.f;
+      if (co < cout && k < K) {
+        const int tap = k / cin, ci = k - tap * cin;
+        v = layout ? wt[((size_t)tap * cout + co) * cin + ci] : wt[((size_t)tap * cin + ci) * cout + co];
+      }
+      _Float16 h, l;
+      split1(v * s, h, l);
+      hi[j] = h;
+      lo[j] = l;
+    }
+    wp[(size_t)(ct * 2 + 0) * 64 + lane] = hi;
+    wp[(size_t)(ct * 2 + 1) * 64 + lane] = lo;
+  }
+}
+
 // NT = output channels per block (16, 32 or 64); VEC: cin % 32 == 0 (a K chunk is 32
-// consecutive channels of one tap: two float4 per thread), else one element per (pixel, k)
-template <int NT, bool VEC>
+// consecutive channels of one tap: two float4 per thread, stored as f16x4 hi / lo), else one
+// element per (pixel, k); PH (VEC, transposed, stride 2): the block's pixels share one output
+// phase and the K loop visits only that phase's taps (a quarter of them).  The weights'
+// A fragments come straight from the packed buffer (one chunk ahead in registers); only the
+// gathered activations go through LDS.
+template <int NT, bool VEC, bool PH>
 __global__ __launch_bounds__(256) void conv_gather_kernel(GatherArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 xs[2][GM * LP];  // [hi, lo][pixel][k]
-  __shared__ __attribute__((aligned(16))) _Float16 ws[2][NT * LP];  // [hi, lo][co][k]
   constexpr int NTT = NT / 16;
-  constexpr int XN = VEC ? 2 : 8;               // x elements (float4s when VEC) per thread per chunk
-  constexpr int WN = NT * TK / 256;             // weight elements per thread per chunk
+  constexpr int XN = VEC ? 2 : 8;  // x elements (float4s when VEC) per thread per chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
-  const long long m0 = (long long)blockIdx.x * GM;
+  int phase = 0, blk = blockIdx.x;
+  if constexpr (PH) {
+    while (phase < 3 && blk >= a.ph_blk[phase + 1]) ++phase;
+    blk -= a.ph_blk[phase];
+  }
+  const int py = phase >> 1, px = phase & 1;
+  const long long m0 = (long long)blk * GM;
   const float sx = ld_scale(a.sx), sw = ld_scale(a.sw);
-  const int nchunk = (a.K + TK - 1) / TK;
+  // K chunks: all of them, or (PH) the phase's taps ky = ky0 + 2 i, kx = kx0 + 2 j
+  const int cc_n = VEC ? a.cin / TK : 1;
+  const int ky0 = (py + a.pad_y) & 1, kx0 = (px + a.pad_x) & 1;
+  const int tny = (a.kh - ky0 + 1) >> 1, tnx = (a.kw - kx0 + 1) >> 1;
+  const int nchunk = PH ? tny * tnx * cc_n : (a.K + TK - 1) / TK;
+  auto chunk_tap = [&](int c, int& ky, int& kx, int& ci0, int& gc) {  // VEC: tap and channel block of chunk c
+    if constexpr (PH) {
+      const int tt = c / cc_n, cc = c - tt * cc_n, iy = tt / tnx;
+      ky = ky0 + 2 * iy;
+      kx = kx0 + 2 * (tt - iy * tnx);
+      ci0 = cc * TK;
+      gc = (ky * a.kw + kx) * cc_n + cc;
+    } else {
+      const int k0 = c * TK, tap = k0 / a.cin;
+      ky = tap / a.kw;
+      kx = tap - ky * a.kw;
+      ci0 = k0 - tap * a.cin;
+      gc = c;
+    }
+  };
+
   // this thread's staging pixels: VEC px = tid/8 + 32 r; scalar px = tid/32 + 8 e
-  int pb[XN], py[XN], pxx[XN];
+  int pb[XN], pyy[XN], pxx[XN];
 #pragma unroll
   for (int e = 0; e < XN; ++e) {
-    const int px = VEC ? (tid >> 3) + 32 * e : (tid >> 5) + 8 * e;
-    const long long m = m0 + px;
-    if (m < a.M) {
-      const long long per = (long long)a.oh * a.ow;
-      pb[e] = (int)(m / per);
-      const int r = (int)(m - (long long)pb[e] * per);
-      py[e] = r / a.ow;
-      pxx[e] = r - py[e] * a.ow;
-    } else {
-      pb[e] = -1;
-      py[e] = pxx[e] = 0;
-    }
+    const int sp = VEC ? (tid >> 3) + 32 * e : (tid >> 5) + 8 * e;
+    if (!pixel_of(a, PH, py, px, m0 + sp, pb[e], pyy[e], pxx[e])) pb[e] = -1;
   }
 
   f32x4 xv[VEC ? XN : 1];
   float xsv[VEC ? 1 : XN];
-  float wv[WN];
-  auto load = [&](int c) {
-    const int k0 = c * TK;
+  f16x8 wc[NTT][2], wn[NTT][2];  // A fragments of the current / next chunk (static indices: no scratch)
+  auto load = [&](int c, f16x8 (&w)[NTT][2]) {
+    int ky, kx, ci0, gc;
     if constexpr (VEC) {
-      const int tap = k0 / a.cin, ci0 = k0 - tap * a.cin, ky = tap / a.kw, kx = tap - ky * a.kw;
+      chunk_tap(c, ky, kx, ci0, gc);
 #pragma unroll
       for (int e = 0; e < XN; ++e) {
-        const long long s = pb[e] >= 0 ? gather_src(a, pb[e], py[e], pxx[e], ky, kx) : -1;
+        const long long s = pb[e] >= 0 ? gather_src(a, pb[e], pyy[e], pxx[e], ky, kx) : -1;
         xv[e] = s >= 0 ? *(const f32x4*)(a.x + s * a.cin + ci0 + 4 * (tid & 7)) : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     } else {
-      const int k = k0 + (tid & 31);
-      const int tap = k / a.cin, ci = k - tap * a.cin, ky = tap / a.kw, kx = tap - ky * a.kw;
+      gc = c;
+      const int k = c * TK + (tid & 31);
+      const int tap = k / a.cin, ci = k - tap * a.cin;
+      ky = tap / a.kw;
+      kx = tap - ky * a.kw;
 #pragma unroll
       for (int e = 0; e < XN; ++e) {
-        const long long s = (pb[e] >= 0 && k < a.K) ? gather_src(a, pb[e], py[e], pxx[e], ky, kx) : -1;
+        const long long s = (pb[e] >= 0 && k < a.K) ? gather_src(a, pb[e], pyy[e], pxx[e], ky, kx) : -1;
         xsv[e] = s >= 0 ? a.x[s * a.cin + ci] : 0.f;
       }
     }
 #pragma unroll
-    for (int e = 0; e < WN; ++e) {
-      const int idx = tid + 256 * e;
-      // layout 0: co fastest (contiguous in [tap][ci][co]); layout 1: k fastest ([tap][co][ci])
-      const int co = a.layout ? idx / TK : idx % NT, kk = a.layout ? idx % TK : idx / NT;
-      const int k = k0 + kk;
-      float v = 0.f;
-      if (co < a.cout && k < a.K) {
-        const int tap = k / a.cin, ci = k - tap * a.cin;
-        v = a.layout ? a.wt[((size_t)tap * a.cout + co) * a.cin + ci] : a.wt[((size_t)tap * a.cin + ci) * a.cout + co];
-      }
-      wv[e] = v;
-    }
+    for (int t = 0; t < NTT; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) w[t][hl] = a.wp[((size_t)(gc * NTT + t) * 2 + hl) * 64 + lane];
   };
   auto stage = [&]() {
     if constexpr (VEC) {
+      typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
 #pragma unroll
       for (int e = 0; e < XN; ++e) {
-        const int px = (tid >> 3) + 32 * e, k = 4 * (tid & 7);
+        const int sp = (tid >> 3) + 32 * e, k = 4 * (tid & 7);
+        f16x4v hi, lo;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) split1(xv[e][r] * sx, xs[0][px * LP + k + r], xs[1][px * LP + k + r]);
+        for (int r = 0; r < 4; ++r) {
+          _Float16 h, l;
+          split1(xv[e][r] * sx, h, l);
+          hi[r] = h;
+          lo[r] = l;
+        }
+        *(f16x4v*)&xs[0][sp * LP + k] = hi;
+        *(f16x4v*)&xs[1][sp * LP + k] = lo;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < XN; ++e) {
-        const int px = (tid >> 5) + 8 * e, k = tid & 31;
-        split1(xsv[e] * sx, xs[0][px * LP + k], xs[1][px * LP + k]);
+        const int sp = (tid >> 5) + 8 * e, k = tid & 31;
+        split1(xsv[e] * sx, xs[0][sp * LP + k], xs[1][sp * LP + k]);
       }
-    }
-#pragma unroll
-    for (int e = 0; e < WN; ++e) {
-      const int idx = tid + 256 * e;
-      const int co = a.layout ? idx / TK : idx % NT, kk = a.layout ? idx % TK : idx / NT;
-      split1(wv[e] * sw, ws[0][co * LP + kk], ws[1][co * LP + kk]);
     }
   };
 
   f32x4 acc[NTT];
 #pragma unroll
   for (int t = 0; t < NTT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  load(0);
+  if (nchunk > 0) load(0, wc);
   for (int c = 0; c < nchunk; ++c) {
-    __syncthreads();  // every wave is done with the previous chunk's tiles
+    __syncthreads();  // every wave is done with the previous chunk's tile
     stage();
     __syncthreads();
-    if (c + 1 < nchunk) load(c + 1);  // in flight during this chunk's MFMAs
+    if (c + 1 < nchunk) load(c + 1, wn);  // in flight during this chunk's MFMAs
     const int bo = (wave * 16 + l16) * LP + 8 * g;
     const f16x8 bh = *(const f16x8*)&xs[0][bo], bl = *(const f16x8*)&xs[1][bo];
 #pragma unroll
     for (int t = 0; t < NTT; ++t) {
-      const int ao = (t * 16 + l16) * LP + 8 * g;
-      const f16x8 ah = *(const f16x8*)&ws[0][ao], al = *(const f16x8*)&ws[1][ao];
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[t][1], bh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[t][0], bl, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[t][0], bh, acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) {
+      wc[t][0] = wn[t][0];
+      wc[t][1] = wn[t][1];
     }
   }
   // D[co = 16t + 4g + r][pixel 16 wave + l16]
-  const long long m = m0 + wave * 16 + l16;
-  if (m >= a.M) return;
+  int b, oy, ox;
+  if (!pixel_of(a, PH, py, px, m0 + wave * 16 + l16, b, oy, ox)) return;
   const float isx = 1.0f / sx, isw = 1.0f / sw;  // exact: powers of two (applied one at a time)
-  float* yp = a.y + m * a.cout;
+  float* yp = a.y + (((long long)b * a.oh + oy) * a.ow + ox) * a.cout;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     const int co = t * 16 + 4 * g;
@@ -209,65 +281,113 @@ __global__ __launch_bounds__(256) void conv_gather_kernel(GatherArgs a) {
   }
 }
 
+// ---- separable Gaussian of the SSIM loss (tf.image.ssim's 11-tap window) --------------------
+// One-channel planes (n, h, w): VALID correlation along x (vertical = 0) or y, or its adjoint
+// (the input gradient: a full convolution with the same taps).
+__global__ __launch_bounds__(256) void gauss1d_kernel(const float* __restrict__ in, int n, int hi, int wi,
+                                                      const float* __restrict__ taps, int nt, int vertical, int adjoint,
+                                                      float* __restrict__ out, int ho, int wo) {
+  const long long total = (long long)n * ho * wo;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int x = (int)(i % wo);
+    const long long r = i / wo;
+    const int y = (int)(r % ho), b = (int)(r / ho);
+    const float* src = in + (long long)b * hi * wi;
+    float s = 0.f;
+    for (int k = 0; k < nt; ++k) {
+      const int yy = vertical ? (adjoint ? y - k : y + k) : y;
+      const int xx = vertical ? x : (adjoint ? x - k : x + k);
+      if ((unsigned)yy < (unsigned)hi && (unsigned)xx < (unsigned)wi) s = fmaf(taps[k], src[(long long)yy * wi + xx], s);
+    }
+    out[i] = s;
+  }
+}
+
 // ---- weight-gradient GEMM ------------------------------------------------------------------
 struct WgradArgs {
   const float* gat;   // [n][gh][gw][ca], read at s*u + k - pad
   const float* dir;   // [n][uh][uw][cb]
   const float* sg;    // device scales or null
   const float* sd;
-  float* part;        // [slices][taps][ca][cb]
+  float* part;        // [slices][taps * ca rows][cb]
   int n, gh, gw, ca, uh, uw, cb, kh, kw, stride, pad_y, pad_x;
+  int rows;           // taps * ca: the GEMM's M (row r = tap * ca + a)
   long long U;        // n * uh * uw
   int slice_len;      // pixels per slice (multiple of TK)
 };
 
-// NA, NB = channel tiles (16, 32, 64) >= ca, cb.  Block (tap, slice); wave w owns the
-// (a, b) 16 x 16 output tiles w, w + 4, ...
+// M = (tap, a) rows flattened (r = tap * ca + a), N = b, K = the slice's pixels.  NA rows
+// per block (16 ... 64: one tap of a 64-channel gat, two taps of a 32-channel one, or all
+// 25 taps of a one-channel one), NB >= cb; block (row block, slice) stages the dir
+// tile once for all its rows; wave w owns the 16 x 16 output tiles w, w + 4, ...
 template <int NA, int NB>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 gs[2][NA * LP];  // [hi, lo][a][u]
-  __shared__ __attribute__((aligned(16))) _Float16 ds[2][NB * LP];  // [hi, lo][b][u]
+  constexpr int NMAX = NA > NB ? NA : NB;
+  __shared__ __attribute__((aligned(16))) _Float16 gs[2][NMAX * LP];  // [hi, lo][a][u]
+  __shared__ __attribute__((aligned(16))) _Float16 ds[2][NMAX * LP];  // [hi, lo][b][u]
   constexpr int NTA = NA / 16, NTB = NB / 16, NTILE = NTA * NTB, TPW = (NTILE + 3) / 4;
-  constexpr int GE = (TK * NA + 255) / 256, DE = (TK * NB + 255) / 256;  // elements per thread
+  // staging: thread item = (channel, 4 consecutive pixels u): 4 loads coalesced across the
+  // channel-contiguous lanes, one f16x4 hi and one lo store into the [channel][u] tiles
+  constexpr int GE = (TK / 4 * NA + 255) / 256, DE = (TK / 4 * NB + 255) / 256;
+  typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
-  const int tap = blockIdx.x, slice = blockIdx.y, ky = tap / a.kw, kx = tap - ky * a.kw;
+  const int r0 = blockIdx.x * NA, slice = blockIdx.y;
   const long long u0 = (long long)slice * a.slice_len;
   const long long u1 = u0 + a.slice_len < a.U ? u0 + a.slice_len : a.U;
   const float sg = ld_scale(a.sg), sd = ld_scale(a.sd);
   const long long per = (long long)a.uh * a.uw;
 
-  float gv[GE], dv[DE];
+  f32x4 gv[GE], dv[DE];
   auto load = [&](long long ub) {
 #pragma unroll
-    for (int e = 0; e < GE; ++e) {  // element (u = idx / NA, channel idx % NA): channels fastest
-      const int idx = tid + 256 * e, ul = idx / NA, ch = idx % NA;
-      const long long u = ub + ul;
-      float v = 0.f;
-      if (idx < TK * NA && ch < a.ca && u < u1) {
-        const int b = (int)(u / per), r = (int)(u - (long long)b * per), uy = r / a.uw, ux = r - uy * a.uw;
-        const int iy = a.stride * uy + ky - a.pad_y, ix = a.stride * ux + kx - a.pad_x;
-        if ((unsigned)iy < (unsigned)a.gh && (unsigned)ix < (unsigned)a.gw)
-          v = a.gat[(((size_t)b * a.gh + iy) * a.gw + ix) * a.ca + ch];
+    for (int e = 0; e < GE; ++e) {
+      const int idx = tid + 256 * e, ug = idx / NA, row = r0 + idx % NA;
+      const int tap = row / a.ca, ch = row - tap * a.ca, ky = tap / a.kw, kx = tap - ky * a.kw;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long u = ub + 4 * ug + i;
+        float v = 0.f;
+        if (idx < TK / 4 * NA && row < a.rows && u < u1) {
+          const int b = (int)(u / per), r = (int)(u - (long long)b * per), uy = r / a.uw, ux = r - uy * a.uw;
+          const int iy = a.stride * uy + ky - a.pad_y, ix = a.stride * ux + kx - a.pad_x;
+          if ((unsigned)iy < (unsigned)a.gh && (unsigned)ix < (unsigned)a.gw)
+            v = a.gat[(((size_t)b * a.gh + iy) * a.gw + ix) * a.ca + ch];
+        }
+        gv[e][i] = v;
       }
-      gv[e] = v;
     }
 #pragma unroll
     for (int e = 0; e < DE; ++e) {
-      const int idx = tid + 256 * e, ul = idx / NB, ch = idx % NB;
-      const long long u = ub + ul;
-      dv[e] = (idx < TK * NB && ch < a.cb && u < u1) ? a.dir[u * a.cb + ch] : 0.f;
+      const int idx = tid + 256 * e, ug = idx / NB, ch = idx % NB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long u = ub + 4 * ug + i;
+        dv[e][i] = (idx < TK / 4 * NB && ch < a.cb && u < u1) ? a.dir[u * a.cb + ch] : 0.f;
+      }
     }
+  };
+  auto put = [&](_Float16 (&tile)[2][(NA > NB ? NA : NB) * LP], int row, int col, const f32x4& v, float s) {
+    f16x4v hi, lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      _Float16 h, l;
+      split1(v[i] * s, h, l);
+      hi[i] = h;
+      lo[i] = l;
+    }
+    *(f16x4v*)&tile[0][row * LP + col] = hi;
+    *(f16x4v*)&tile[1][row * LP + col] = lo;
   };
   auto stage = [&]() {
 #pragma unroll
     for (int e = 0; e < GE; ++e) {
       const int idx = tid + 256 * e;
-      if (idx < TK * NA) split1(gv[e] * sg, gs[0][(idx % NA) * LP + idx / NA], gs[1][(idx % NA) * LP + idx / NA]);
+      if (idx < TK / 4 * NA) put(gs, idx % NA, 4 * (idx / NA), gv[e], sg);
     }
 #pragma unroll
     for (int e = 0; e < DE; ++e) {
       const int idx = tid + 256 * e;
-      if (idx < TK * NB) split1(dv[e] * sd, ds[0][(idx % NB) * LP + idx / NB], ds[1][(idx % NB) * LP + idx / NB]);
+      if (idx < TK / 4 * NB) put(ds, idx % NB, 4 * (idx / NB), dv[e], sd);
     }
   };
 
@@ -294,8 +414,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     }
   }
   const float isg = 1.0f / sg, isd = 1.0f / sd;
-  const int taps = a.kh * a.kw;
-  float* out = a.part + ((size_t)slice * taps + tap) * a.ca * a.cb;
+  float* out = a.part + ((size_t)slice * a.rows + r0) * a.cb;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int t = wave + 4 * j;
@@ -304,17 +423,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int arow = ta * 16 + 4 * g + r;
-      if (arow < a.ca && bcol < a.cb) out[(size_t)arow * a.cb + bcol] = (acc[j][r] * isg) * isd;
+      if (r0 + arow < a.rows && bcol < a.cb) out[(size_t)arow * a.cb + bcol] = (acc[j][r] * isg) * isd;
     }
   }
 }
 
-// dw[i] = sum over slices of part[s][i], in slice order
+// dw[i] = sum over slices of part[s][i]: 8 independent loads in flight per thread, summed
+// in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int slices, long long nw,
                                                            float* __restrict__ dw) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nw; i += (long long)gridDim.x * 256) {
     float s = 0.f;
-    for (int k = 0; k < slices; ++k) s += part[(size_t)k * nw + i];
+    int k = 0;
+    for (; k + 8 <= slices; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(size_t)(k + j) * nw + i];
+      s += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    }
+    for (; k < slices; ++k) s += part[(size_t)k * nw + i];
     dw[i] = s;
   }
 }
@@ -354,16 +481,16 @@ __global__ __launch_bounds__(256) void scale_finish_kernel(const float* __restri
   }
 }
 
-template <int NT, bool VEC>
+template <int NT, bool VEC, bool PH>
 hipError_t launch_gather_t(const GatherArgs& a, hipStream_t st) {
-  const long long blocks = (a.M + GM - 1) / GM;
-  hipLaunchKernelGGL((conv_gather_kernel<NT, VEC>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const long long blocks = PH ? a.ph_blk[4] : (a.M + GM - 1) / GM;
+  hipLaunchKernelGGL((conv_gather_kernel<NT, VEC, PH>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 template <int NA, int NB>
 hipError_t launch_wgrad_t(const WgradArgs& a, int slices, hipStream_t st) {
-  hipLaunchKernelGGL((conv_wgrad_kernel<NA, NB>), dim3(a.kh * a.kw, slices), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_wgrad_kernel<NA, NB>), dim3((a.rows + NA - 1) / NA, slices), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -383,31 +510,74 @@ hipError_t launch_absmax_scale(const float* x, long long n, float* scale, float*
   return hipGetLastError();
 }
 
+size_t train_gather_work_bytes(int kh, int kw, int cin, int cout) {
+  return (size_t)((kh * kw * cin + TK - 1) / TK) * (tile16(cout) / 16) * 2 * 64 * sizeof(f16x8);
+}
+
 hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int layout,
-                              int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* scales,
-                              float* y, int oh, int ow, int cout, hipStream_t st) {
+                              int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                              const float* w_scale, float* y, int oh, int ow, int cout, void* work, hipStream_t st) {
   GatherArgs a{};
-  a.x = x; a.wt = wt; a.bias = bias; a.y = y;
-  a.sx = scales; a.sw = scales ? scales + 1 : nullptr;
+  a.x = x; a.wp = (const f16x8*)work; a.bias = bias; a.y = y;
+  a.sx = x_scale; a.sw = w_scale;
   a.n = n; a.h = h; a.w = w; a.cin = cin; a.oh = oh; a.ow = ow; a.cout = cout; a.kh = kh; a.kw = kw;
-  a.stride = stride; a.pad_y = pad_y; a.pad_x = pad_x; a.transposed = transposed; a.layout = layout;
+  a.stride = stride; a.pad_y = pad_y; a.pad_x = pad_x; a.transposed = transposed;
   a.K = kh * kw * cin;
   a.M = (long long)n * oh * ow;
   if (a.M == 0) return hipSuccess;
+  const int ntt = tile16(cout) / 16, nchunk = (a.K + TK - 1) / TK;
+  {
+    const int total = nchunk * ntt * 64;
+    hipLaunchKernelGGL(pack_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, wt, layout, cin, cout, a.K, ntt,
+                       nchunk, w_scale, (f16x8*)work);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   const bool vec = cin % TK == 0 && ((uintptr_t)x & 15) == 0;
-  switch (tile16(cout) | (vec ? 1 : 0)) {
-    case 16: return launch_gather_t<16, false>(a, st);
-    case 17: return launch_gather_t<16, true>(a, st);
-    case 32: return launch_gather_t<32, false>(a, st);
-    case 33: return launch_gather_t<32, true>(a, st);
-    case 64: return launch_gather_t<64, false>(a, st);
-    default: return launch_gather_t<64, true>(a, st);
+  const bool ph = vec && transposed && stride == 2;
+  if (ph) {  // blocks per output phase
+    a.ph_blk[0] = 0;
+    for (int p = 0; p < 4; ++p) {
+      const long long qh = (oh - (p >> 1) + 1) / 2, qw = (ow - (p & 1) + 1) / 2;
+      a.ph_blk[p + 1] = a.ph_blk[p] + (int)((n * qh * qw + GM - 1) / GM);
+    }
+    if (a.ph_blk[4] == 0) return hipSuccess;
+  }
+  switch (tile16(cout) | (vec ? 1 : 0) | (ph ? 2 : 0)) {
+    case 16: return launch_gather_t<16, false, false>(a, st);
+    case 17: return launch_gather_t<16, true, false>(a, st);
+    case 19: return launch_gather_t<16, true, true>(a, st);
+    case 32: return launch_gather_t<32, false, false>(a, st);
+    case 33: return launch_gather_t<32, true, false>(a, st);
+    case 35: return launch_gather_t<32, true, true>(a, st);
+    case 64: return launch_gather_t<64, false, false>(a, st);
+    case 65: return launch_gather_t<64, true, false>(a, st);
+    default: return launch_gather_t<64, true, true>(a, st);
   }
 }
 
-// slices so that taps x slices fills the chip several times over, each slice >= 4 chunks
-static int wgrad_slices(long long U, int taps) {
-  long long want = (2048 + taps - 1) / taps;
+hipError_t launch_gauss1d(const float* in, int n, int hi, int wi, const float* taps, int nt, int vertical, int adjoint,
+                          float* out, int ho, int wo, hipStream_t st) {
+  const long long total = (long long)n * ho * wo;
+  if (total == 0) return hipSuccess;
+  const long long blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(gauss1d_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, st, in, n, hi,
+                     wi, taps, nt, vertical, adjoint, out, ho, wo);
+  return hipGetLastError();
+}
+
+// rows per block: 64 (one tap of a 64-channel gat, two of a 32-channel one) / 32 / 16 rows
+// (all 25 taps of a one-channel gat)
+static int wgrad_na(int taps, int ca) {
+  const int rows = taps * ca;
+  (void)taps;
+  return rows > 32 ? 64 : rows > 16 ? 32 : 16;  // (two taps of 64 channels per block, NA 128: measured 35 % slower)
+}
+
+// slices so that row blocks x slices fills the chip about eight times over, each slice
+// >= 4 chunks
+static int wgrad_slices(long long U, int rowblocks) {
+  long long want = (2048 + rowblocks - 1) / rowblocks;
   const long long maxs = (U + 4 * TK - 1) / (4 * TK);
   if (want > maxs) want = maxs;
   return (int)(want < 1 ? 1 : want);
@@ -415,14 +585,15 @@ static int wgrad_slices(long long U, int taps) {
 
 size_t train_wgrad_work_floats(int n, int uh, int uw, int kh, int kw, int ca, int cb) {
   const long long U = (long long)n * uh * uw;
-  return (size_t)wgrad_slices(U, kh * kw) * kh * kw * ca * cb;
+  const int rows = kh * kw * ca, na = wgrad_na(kh * kw, ca);
+  return (size_t)wgrad_slices(U, (rows + na - 1) / na) * rows * cb;
 }
 
 hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb,
-                             int kh, int kw, int stride, int pad_y, int pad_x, const float* scales, float* dw,
-                             float* work, hipStream_t st) {
+                             int kh, int kw, int stride, int pad_y, int pad_x, const float* gat_scale,
+                             const float* dir_scale, float* dw, float* work, hipStream_t st) {
   WgradArgs a{};
-  a.gat = gat; a.dir = dir; a.sg = scales; a.sd = scales ? scales + 1 : nullptr;
+  a.gat = gat; a.dir = dir; a.sg = gat_scale; a.sd = dir_scale;
   a.part = work;
   a.n = n; a.gh = gh; a.gw = gw; a.ca = ca; a.uh = uh; a.uw = uw; a.cb = cb; a.kh = kh; a.kw = kw;
   a.stride = stride; a.pad_y = pad_y; a.pad_x = pad_x;
@@ -431,18 +602,20 @@ hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, co
   const long long nw = (long long)taps * ca * cb;
   if (nw == 0) return hipSuccess;
   if (a.U == 0) return hipMemsetAsync(dw, 0, nw * sizeof(float), st);
-  const int slices = wgrad_slices(a.U, taps);
+  a.rows = taps * ca;
+  const int na = wgrad_na(taps, ca);
+  const int slices = wgrad_slices(a.U, (a.rows + na - 1) / na);
   a.slice_len = (int)(((a.U + slices - 1) / slices + TK - 1) / TK * TK);
   hipError_t e;
-  switch (tile16(ca) * 100 + tile16(cb)) {
-    case 1616: e = launch_wgrad_t<16, 16>(a, slices, st); break;
-    case 1632: e = launch_wgrad_t<16, 32>(a, slices, st); break;
-    case 1664: e = launch_wgrad_t<16, 64>(a, slices, st); break;
-    case 3216: e = launch_wgrad_t<32, 16>(a, slices, st); break;
-    case 3232: e = launch_wgrad_t<32, 32>(a, slices, st); break;
-    case 3264: e = launch_wgrad_t<32, 64>(a, slices, st); break;
-    case 6416: e = launch_wgrad_t<64, 16>(a, slices, st); break;
-    case 6432: e = launch_wgrad_t<64, 32>(a, slices, st); break;
+  switch (na * 1000 + tile16(cb)) {
+    case 16016: e = launch_wgrad_t<16, 16>(a, slices, st); break;
+    case 16032: e = launch_wgrad_t<16, 32>(a, slices, st); break;
+    case 16064: e = launch_wgrad_t<16, 64>(a, slices, st); break;
+    case 32016: e = launch_wgrad_t<32, 16>(a, slices, st); break;
+    case 32032: e = launch_wgrad_t<32, 32>(a, slices, st); break;
+    case 32064: e = launch_wgrad_t<32, 64>(a, slices, st); break;
+    case 64016: e = launch_wgrad_t<64, 16>(a, slices, st); break;
+    case 64032: e = launch_wgrad_t<64, 32>(a, slices, st); break;
     default: e = launch_wgrad_t<64, 64>(a, slices, st); break;
   }
   if (e != hipSuccess) return e;

@@ -13,11 +13,11 @@ Conv2DTranspose dx     gather, src = s*o + k - pad, same kernel (layout 0)
 Conv2DTranspose dW     wgrad(gat = dy, dir = x) -> HWOI
 =====================  ==========================================================
 
-The SSIM loss's separable Gaussian (one-channel VALID correlation) runs on the same gather
-kernel (``gauss_valid``).
+The SSIM loss's separable Gaussian (one-channel VALID correlation) runs on a 1-D HIP
+kernel and its adjoint (``gauss_valid``, ``nic_gauss_1d``).
 
 Each operand gets a power-of-two scale (max |t| * scale in [2^13, 2^14)) computed on the
-device, so the f16 hi/lo split keeps tiny gradients exact to ~2^-22.  Bias gradients are
+device once per tensor (x and the kernel in the forward, dy in the backward), so the f16 hi/lo split keeps tiny gradients exact to ~2^-22.  Bias gradients are
 plain reductions (torch), as are the leaky-ReLU / clip / SSIM elementwise parts.  There is
 no fallback: without the built library these raise.
 """
@@ -44,16 +44,14 @@ def _stream():
     return _torch().cuda.current_stream().cuda_stream
 
 
-def _scales(*ts):
-    """Device (len(ts),) fp32 tensor of power-of-two operand scales (nic_absmax_scale)."""
+def scale(t):
+    """Device (1,) fp32 power-of-two operand scale of t (nic_absmax_scale); computed once per
+    tensor and passed to every GEMM that reads it."""
     torch = _torch()
-    dev = ts[0].device
-    out = torch.empty(len(ts), dtype=torch.float32, device=dev)
-    work = torch.empty(512, dtype=torch.float32, device=dev)
-    L = _lib.lib()
-    for i, t in enumerate(ts):
-        _lib.check(L.nic_absmax_scale(t.data_ptr(), t.numel(), out.data_ptr() + 4 * i, work.data_ptr(), _stream()),
-                   "nic_absmax_scale")
+    out = torch.empty(1, dtype=torch.float32, device=t.device)
+    work = torch.empty(512, dtype=torch.float32, device=t.device)
+    _lib.check(_lib.lib().nic_absmax_scale(t.data_ptr(), t.numel(), out.data_ptr(), work.data_ptr(), _stream()),
+               "nic_absmax_scale")
     return out
 
 
@@ -65,23 +63,31 @@ def _check(t, name):
 
 
 def gather(x, wt, layout: int, stride: int, pad: Tuple[int, int], transposed: int, out_hw: Tuple[int, int],
-           cout: int, bias=None):
-    """nic_conv_gather on NHWC x: returns (n, oh, ow, cout)."""
+           cout: int, bias=None, sx=None, sw=None):
+    """nic_conv_gather on NHWC x: returns (n, oh, ow, cout).  sx / sw: operand scales
+    (:func:`scale`), computed here when not given."""
     torch = _torch()
+    import ctypes
+
     x = _check(x, "gather x")
     wt = _check(wt, "gather wt")
     n, h, w, cin = x.shape
     kh, kw = wt.shape[0], wt.shape[1]
+    L = _lib.lib()
+    need = ctypes.c_int64()
+    _lib.check(L.nic_conv_gather_work(kh, kw, cin, cout, ctypes.byref(need)), "nic_conv_gather_work")
+    work = torch.empty(int(need.value) // 4, dtype=torch.float32, device=x.device)
     y = torch.empty((n, out_hw[0], out_hw[1], cout), dtype=torch.float32, device=x.device)
-    sc = _scales(x, wt)
+    sx = scale(x) if sx is None else sx
+    sw = scale(wt) if sw is None else sw
     b = _check(bias, "gather bias").data_ptr() if bias is not None else None
-    _lib.check(_lib.lib().nic_conv_gather(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0],
-                                          pad[1], transposed, b, sc.data_ptr(), y.data_ptr(), out_hw[0], out_hw[1],
-                                          cout, _stream()), "nic_conv_gather")
+    _lib.check(L.nic_conv_gather(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0], pad[1],
+                                 transposed, b, sx.data_ptr(), sw.data_ptr(), y.data_ptr(), out_hw[0], out_hw[1],
+                                 cout, work.data_ptr(), int(need.value), _stream()), "nic_conv_gather")
     return y
 
 
-def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int]):
+def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int], sg=None, sd=None):
     """nic_conv_wgrad: (kh, kw, ca, cb) = sum_u gat[s*u + k - pad][a] * dir[u][b]."""
     torch = _torch()
     import ctypes
@@ -95,11 +101,26 @@ def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int]):
     _lib.check(L.nic_conv_wgrad_work(n, uh, uw, kh, kw, ca, cb, ctypes.byref(need)), "nic_conv_wgrad_work")
     work = torch.empty(max(int(need.value), 1), dtype=torch.float32, device=gat.device)
     dw = torch.empty((kh, kw, ca, cb), dtype=torch.float32, device=gat.device)
-    sc = _scales(gat, dirt)
+    sg = scale(gat) if sg is None else sg
+    sd = scale(dirt) if sd is None else sd
     _lib.check(L.nic_conv_wgrad(gat.data_ptr(), n, gh, gw, ca, dirt.data_ptr(), uh, uw, cb, kh, kw, stride, pad[0],
-                                pad[1], sc.data_ptr(), dw.data_ptr(), work.data_ptr(), int(need.value), _stream()),
-               "nic_conv_wgrad")
+                                pad[1], sg.data_ptr(), sd.data_ptr(), dw.data_ptr(), work.data_ptr(), int(need.value),
+                                _stream()), "nic_conv_wgrad")
     return dw
+
+
+def gauss_1d(t, taps, vertical: int, adjoint: int):
+    """nic_gauss_1d on one-channel planes (n, h, w)."""
+    torch = _torch()
+    t = _check(t, "gauss t")
+    n, h, w = t.shape
+    d = taps.numel() - 1
+    sgn = 1 if adjoint else -1
+    ho, wo = (h + sgn * d, w) if vertical else (h, w + sgn * d)
+    out = torch.empty((n, ho, wo), dtype=torch.float32, device=t.device)
+    _lib.check(_lib.lib().nic_gauss_1d(t.data_ptr(), n, h, w, _check(taps, "gauss taps").data_ptr(), taps.numel(),
+                                       vertical, adjoint, out.data_ptr(), ho, wo, _stream()), "nic_gauss_1d")
+    return out
 
 
 def _conv_fn():
@@ -114,19 +135,21 @@ def _conv_fn():
             kh, kw, _, cout = kernel.shape
             pt, pl = same_pad(h, kh, stride)[0], same_pad(w, kw, stride)[0]
             oh, ow = -(-h // stride), -(-w // stride)
-            ctx.save_for_backward(x, kernel)
+            sx, sw = scale(x), scale(kernel)
+            ctx.save_for_backward(x, kernel, sx, sw)
             ctx.geo = (stride, pt, pl)
-            return gather(x, kernel, 0, stride, (pt, pl), 0, (oh, ow), cout, bias)
+            return gather(x, kernel, 0, stride, (pt, pl), 0, (oh, ow), cout, bias, sx, sw)
 
         @staticmethod
         def backward(ctx, dy):
-            x, kernel = ctx.saved_tensors
+            x, kernel, sx, sw = ctx.saved_tensors
             stride, pt, pl = ctx.geo
             dy = dy.contiguous()
+            sdy = scale(dy)
             kh, kw, cin, _ = kernel.shape
-            dx = gather(dy, kernel, 1, stride, (pt, pl), 1, (x.shape[1], x.shape[2]), cin) \
+            dx = gather(dy, kernel, 1, stride, (pt, pl), 1, (x.shape[1], x.shape[2]), cin, None, sdy, sw) \
                 if ctx.needs_input_grad[0] else None
-            dk = wgrad(x, dy, kh, kw, stride, (pt, pl)) if ctx.needs_input_grad[1] else None
+            dk = wgrad(x, dy, kh, kw, stride, (pt, pl), sx, sdy) if ctx.needs_input_grad[1] else None
             db = dy.sum(dim=(0, 1, 2)) if ctx.needs_input_grad[2] else None
             return dx, dk, db, None
 
@@ -139,40 +162,40 @@ def _conv_fn():
             kh, kw, cout, _ = kernel.shape
             oh, ow = h * stride, w * stride
             pt, pl = same_pad(oh, kh, stride)[0], same_pad(ow, kw, stride)[0]
-            ctx.save_for_backward(x, kernel)
+            sx, sw = scale(x), scale(kernel)
+            ctx.save_for_backward(x, kernel, sx, sw)
             ctx.geo = (stride, pt, pl)
-            return gather(x, kernel, 1, stride, (pt, pl), 1, (oh, ow), cout, bias)
+            return gather(x, kernel, 1, stride, (pt, pl), 1, (oh, ow), cout, bias, sx, sw)
 
         @staticmethod
         def backward(ctx, dy):
-            x, kernel = ctx.saved_tensors
+            x, kernel, sx, sw = ctx.saved_tensors
             stride, pt, pl = ctx.geo
             dy = dy.contiguous()
+            sdy = scale(dy)
             kh, kw, _, cin = kernel.shape
-            dx = gather(dy, kernel, 0, stride, (pt, pl), 0, (x.shape[1], x.shape[2]), cin) \
+            dx = gather(dy, kernel, 0, stride, (pt, pl), 0, (x.shape[1], x.shape[2]), cin, None, sdy, sw) \
                 if ctx.needs_input_grad[0] else None
-            dk = wgrad(dy, x, kh, kw, stride, (pt, pl)) if ctx.needs_input_grad[1] else None
+            dk = wgrad(dy, x, kh, kw, stride, (pt, pl), sdy, sx) if ctx.needs_input_grad[1] else None
             db = dy.sum(dim=(0, 1, 2)) if ctx.needs_input_grad[2] else None
             return dx, dk, db, None
 
-    class Conv2DValid1(torch.autograd.Function):
-        """One-channel VALID correlation with a constant kernel (kh, kw, 1, 1), NHWC: the
+    class Gauss1D(torch.autograd.Function):
+        """One-channel VALID correlation along x or y with constant taps (nic_gauss_1d), the
         separable Gaussian of tf.image.ssim (the SSIM loss, training.py:119-121)."""
 
         @staticmethod
-        def forward(ctx, x, kernel):
-            n, h, w, _ = x.shape
-            kh, kw = kernel.shape[0], kernel.shape[1]
-            ctx.save_for_backward(kernel)
-            ctx.hw = (h, w)
-            return gather(x, kernel, 0, 1, (0, 0), 0, (h - kh + 1, w - kw + 1), 1)
+        def forward(ctx, t, taps, vertical):
+            ctx.save_for_backward(taps)
+            ctx.vertical = vertical
+            return gauss_1d(t, taps, vertical, 0)
 
         @staticmethod
         def backward(ctx, dy):
-            (kernel,) = ctx.saved_tensors
-            return gather(dy.contiguous(), kernel, 1, 1, (0, 0), 1, ctx.hw, 1), None
+            (taps,) = ctx.saved_tensors
+            return gauss_1d(dy.contiguous(), taps, ctx.vertical, 1), None, None
 
-    return Conv2DSame, Conv2DTransposeSame, Conv2DValid1
+    return Conv2DSame, Conv2DTransposeSame, Gauss1D
 
 
 _FNS = None
@@ -201,13 +224,12 @@ def tconv_same(x, kernel_hwoi, bias, stride: int):
 
 
 def gauss_valid(t, g1d):
-    """Separable VALID Gaussian of NCHW one-channel planes (N,1,H,W) on the HIP gather GEMM
+    """Separable VALID Gaussian of NCHW one-channel planes (N,1,H,W) on the HIP 1-D kernel
     (horizontal then vertical, as training.ssim's filt): returns (N,1,H-10,W-10)."""
     n, c, h, w = t.shape
     if c != 1:
         raise ValueError("gauss_valid: one-channel planes")
-    k = g1d.numel()
-    x = t.reshape(n, h, w, 1)
-    x = _fns()[2].apply(x, g1d.reshape(1, k, 1, 1).contiguous())
-    x = _fns()[2].apply(x, g1d.reshape(k, 1, 1, 1).contiguous())
+    g1d = g1d.contiguous()
+    x = _fns()[2].apply(t.reshape(n, h, w), g1d, 0)
+    x = _fns()[2].apply(x, g1d, 1)
     return x.reshape(n, 1, x.shape[1], x.shape[2])
