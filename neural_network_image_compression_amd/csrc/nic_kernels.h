@@ -53,6 +53,7 @@ struct ConvArgs {
   int ws_taps;            // weight-stationary kernels: taps per model in wx
   int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
+  int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
   // conv1 fused into conv2 (f16x3): the colour plane is computed from the RGB input and
   // conv1's split output is written straight into conv2's LDS halo (no HBM round trip)
   const uint8_t* rgb;     // [N][H0][W0][3]

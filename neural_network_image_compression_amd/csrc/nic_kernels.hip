@@ -2263,12 +2263,21 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   range_report(a.rg, rmax);
 }
 
+// XCD-contiguous tile positions (ConvArgs::tile_xcd): block b of a group of nb runs on XCD
+// (base + b) % 8, so give the blocks of one XCD consecutive positions in each round of nb
+// tiles -- neighbouring tiles, whose halos overlap, are then fetched into one L2.
+__device__ __forceinline__ int xcd_pos(int b, int nb) {
+  const int x = b & 7, q = nb >> 3, r = nb & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);  // prefix of the XCD classes before x, then rank
+}
+
 __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
   using G = GeomS2<32, 8, 8>;
   __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
-  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int bi = a.tile_xcd ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
   if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < 4)
     c12_wave<0>(a, lds, gi, bi, nb);
   else
@@ -2285,7 +2294,8 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PP + 256) * 4 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
-  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  const int bi = a.tile_xcd ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
@@ -3446,6 +3456,16 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// XCD-contiguous tile positions in the k5 s2 forward convs (default; NIC_XCD2=0 for the
+// plain block-strided order): conv12 0.2594 -> 0.2572 ms, conv8 0.0767 -> 0.0758 ms same-box
+static bool ws2_tile_xcd() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_XCD2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
 // proportion to their planes.
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
@@ -3467,6 +3487,7 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = (int)by;
   a.ws_blk[2] = (int)(by + bc);
+  a.tile_xcd = ws2_tile_xcd() ? 1 : 0;
   if constexpr (PIPE12)
     hipLaunchKernelGGL(conv12_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   else
@@ -3505,6 +3526,14 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
   return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
 }
 
+static int dconv1_variant() {
+  static const int v = [] {
+    const char* e = getenv("NIC_D1");
+    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : 0;
+  }();
+  return v;
+}
+
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
     case L_CONV2:  // 32->64 k5 s2: tap-split weight-stationary, or 8x8 tile, 2 waves split N
@@ -3521,8 +3550,15 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
                    // quarters, 4x8 tiles), or 4x8 tile with taps split over 4 waves
       if (use_ws()) return launch_ws2<64, 32, 4, 4, OUT_U8_LATENT>(a, st);
       return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_SPLIT, OUT_U8_LATENT, false>(a, st);
-    case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N
-      return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+    case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N (NIC_D1 A/B:
+                    // "16" 8x16 tile, 2 waves x 4 M tiles; "w4" 8x16 tile, 4 waves)
+      switch (dconv1_variant()) {
+        case 1: return launch_x3<32, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        default: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+      }
     case L_DCONV5:
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
       return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
