@@ -91,3 +91,33 @@ def test_create_without_gpu_fails_cleanly():
     rc = _lib.lib().nic_create(0, ctypes.byref(h))
     assert rc < 0 and not h.value
     assert _lib.last_error()
+
+
+def test_training_entry_points_validate_without_a_gpu():
+    # argument checks of the training C-ABI (nic_train.hip) run before any HIP call
+    import ctypes
+
+    L = _lib.lib()
+    b = ctypes.c_int64()
+    assert L.nic_conv_gather_work(5, 5, 32, 64, ctypes.byref(b)) == _lib.NIC_OK
+    assert b.value == ((25 * 32 + 31) // 32) * 4 * 2 * 64 * 16  # chunks x co tiles x hi/lo x lanes x 16 B
+    assert L.nic_conv_gather_work(5, 5, 65, 64, ctypes.byref(b)) == _lib.NIC_ESHAPE  # cin > 64
+    assert L.nic_conv_gather_work(5, 5, 32, 64, None) == _lib.NIC_EINVAL
+    f = ctypes.c_int64()
+    assert L.nic_conv_wgrad_work(4, 32, 32, 3, 3, 64, 64, ctypes.byref(f)) == _lib.NIC_OK
+    assert f.value > 0 and f.value % (9 * 64 * 64) == 0  # whole slices of the (tap, a) x b partials
+    # shape / enum / NULL checks of the GEMMs themselves
+    assert L.nic_conv_gather(None, 1, 8, 8, 0, None, 3, 3, 0, 1, 1, 1, 0, None, None, None, None, 8, 8, 64,
+                             None, 0, None) == _lib.NIC_ESHAPE
+    assert L.nic_conv_gather(None, 1, 8, 8, 64, None, 3, 3, 2, 1, 1, 1, 0, None, None, None, None, 8, 8, 64,
+                             None, 0, None) == _lib.NIC_EINVAL
+    assert L.nic_conv_gather(None, 1, 8, 8, 64, None, 3, 3, 0, 1, 1, 1, 0, None, None, None, None, 8, 8, 64,
+                             None, 0, None) == _lib.NIC_EINVAL
+    assert "NULL" in _lib.last_error()
+    assert L.nic_conv_gather(None, 0, 8, 8, 64, None, 3, 3, 0, 1, 1, 1, 0, None, None, None, None, 8, 8, 64,
+                             None, 0, None) == _lib.NIC_OK  # empty batch: nothing to do
+    assert L.nic_conv_wgrad(None, 1, 8, 8, 64, None, 8, 8, 64, 3, 3, 1, 1, 1, None, None, None, None, 0,
+                            None) == _lib.NIC_EINVAL
+    assert L.nic_gauss_1d(None, 1, 20, 20, None, 11, 0, 0, None, 20, 9, None) == _lib.NIC_ESHAPE  # 20 - 10 != 9
+    assert L.nic_gauss_1d(None, 1, 20, 20, None, 11, 0, 0, None, 20, 10, None) == _lib.NIC_EINVAL
+    assert L.nic_absmax_scale(None, -1, None, None, None) == _lib.NIC_ESHAPE
