@@ -249,10 +249,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device(f"cuda:{local}")
+    # one process per GPU; ranks beyond the visible GPUs share them round-robin (the 1-GPU
+    # test box runs the world > 1 path this way, with NIC_BENCH_BACKEND=gloo)
+    dev_idx = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_idx)
+    device = torch.device(f"cuda:{dev_idx}")
+    backend = os.environ.get("NIC_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
+    coll_dev = device if backend == "nccl" else torch.device("cpu")  # gloo: host tensors
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
         from neural_network_image_compression_amd.parallel import broadcast_weights
         weights = broadcast_weights(W.seeded_weights(0) if rank == 0 else None, dist)  # RCCL, once
     else:
@@ -265,7 +270,7 @@ def main():
     else:
         B, H, W = args.batch or 8, 2160, 3840
     S = args.size
-    codec = Codec(local, precision=args.precision)
+    codec = Codec(dev_idx, precision=args.precision)
     codec.set_weights(weights)
     codec.reserve(B, H, W)
     g = torch.Generator().manual_seed(1000 + rank)
@@ -302,7 +307,7 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
@@ -374,7 +379,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for t in outs:
-            gather_rows(t, world * B, dist, dst=0)
+            gather_rows(t.to(coll_dev), world * B, dist, dst=0)
         torch.cuda.synchronize()
         barrier()
         coll = {"gather_ms": round((time.perf_counter() - t0) * 1e3, 3),
@@ -478,7 +483,7 @@ def main():
     if not args.no_parity and args.workload == "config2":
         out["parity"] = parity_sample(codec, x[:1], weights)
     if not args.no_power_probe and args.workload == "config2" and args.precision == "f16x3":
-        out["roofline"]["power_probe"] = power_probe(local, weights, x, z, r, dom, flops[dom], args.steps, peak)
+        out["roofline"]["power_probe"] = power_probe(dev_idx, weights, x, z, r, dom, flops[dom], args.steps, peak)
     print(json.dumps(out), flush=True)
     barrier()
     torch.cuda.synchronize()

@@ -33,3 +33,29 @@ def test_bench_json_line():
     assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(r) and 0 < r["frac"] < 1
     assert {"value", "unit", "cores", "kind", "sample"} <= set(d["cpu_baseline"])
     assert d["parity"]["psnr_gpu_vs_oracle_db"] >= 50
+
+
+@pytest.mark.gpu
+def test_bench_world2_path_under_torchrun():
+    # bench.py's world > 1 path exactly as the driver launches it (torch.distributed.run, one
+    # process per rank): weight broadcast, MAX-over-ranks timing, the config-3 gather to rank 0,
+    # rank 0's single JSON line.  The GPU box has one GPU, so both ranks share it and the
+    # process group is gloo (NIC_BENCH_BACKEND; RCCL refuses two ranks on one device)
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, NIC_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "4", "--no-power-probe", "--no-host-path", "--no-quality"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["config"]["parallelism"] == "dp2"
+    assert d["value"] > 0 and d["scaling"] == "weak"
+    c = d["collectives"]
+    assert c["gathered_bytes"] == 8 * (32 * 32 * 96 + 256 * 256 * 3)  # latents + recons of both shards
