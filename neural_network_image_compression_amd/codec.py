@@ -295,7 +295,7 @@ class ProClass:
     """utils.py:15-62: shared Y/CbCr model holder (kind 'encoder' or 'decoder')."""
 
     #: chunks of the native host-array pipeline per call (nic_encode_host / nic_decode_host)
-    host_chunks = 3
+    host_chunks = 4
 
     kind = ""
 
