@@ -220,7 +220,8 @@ class Training:
     the target's byte counts may differ from TF's by the two zlib front ends."""
 
     def __init__(self, device: str = "cuda", weights: Optional[W.Weights] = None, seed: int = 0,
-                 checkpoint_dir: str = "../checkpoints/", backend: Optional[str] = None):
+                 checkpoint_dir: str = "../checkpoints/", backend: Optional[str] = None,
+                 png_workers: Optional[int] = None):
         """backend "hip" (default on a GPU): every convolution of the step, forward and
         backward, on the HIP split-f16x3 MFMA kernels (train_hip, NHWC); "torch" (default on
         the CPU): PyTorch autograd convolutions (MIOpen / oneDNN, NCHW) -- the restatement the
@@ -240,7 +241,9 @@ class Training:
         self.entropy_model: Optional[Entropynet] = None
         self._opt = None
         self._gen = torch.Generator(device=self.device).manual_seed(seed)
-        self._pool = ThreadPoolExecutor(max_workers=8)
+        # host threads for the PNG-size target (get_bpp, training.py:14-21: 3B PNG encodes per
+        # step, the step's longest stage); zlib releases the GIL
+        self._pool = ThreadPoolExecutor(max_workers=png_workers or 8)  # 16 measured slower (27.9 vs 32.7 ms per step)
 
     def _model(self, name: str) -> Dict[str, object]:
         pre = name + "/"

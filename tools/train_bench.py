@@ -37,21 +37,26 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--backends", default="hip,torch")
+    ap.add_argument("--png", action="store_true", help="keep the host PNG-size target (the full step)")
+    ap.add_argument("--png-workers", type=int, default=None)
     args = ap.parse_args()
     import torch
 
     from neural_network_image_compression_amd import training as T
     from neural_network_image_compression_amd import weights as W
 
-    T.png_bpp_planes = lambda enc, tot, pool=None: np.zeros(enc.shape[0], np.float32)  # device work only
+    if not args.png:
+        T.png_bpp_planes = lambda enc, tot, pool=None: np.zeros(enc.shape[0], np.float32)  # device work only
     g = torch.Generator().manual_seed(0)
     imgs = torch.randint(0, 256, (args.batch, args.size, args.size, 3), generator=g, dtype=torch.uint8).cuda()
     w0 = W.seeded_weights(0, init="glorot")
     res = {"batch": args.batch, "size": args.size, "steps": args.steps,
            "conv_gflop_fwd": round(conv_gflop(args.batch, args.size), 2),
-           "step": "Training.losses + autograd.grad of the three losses (no Adam, PNG target zeroed)"}
+           "step": "Training.losses + autograd.grad of the three losses (no Adam"
+                   + (", host PNG target)" if args.png else ", PNG target zeroed)")}
     for be in args.backends.split(","):
-        tr = T.Training(device="cuda", weights=w0, seed=0, checkpoint_dir="/tmp/nic_tb/", backend=be)
+        tr = T.Training(device="cuda", weights=w0, seed=0, checkpoint_dir="/tmp/nic_tb/", backend=be,
+                        png_workers=args.png_workers)
 
         def step():
             f = tr.losses(imgs, 0.01, flip=True)
