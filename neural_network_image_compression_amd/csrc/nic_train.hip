@@ -92,9 +92,19 @@ __device__ __forceinline__ long long gather_src(const GatherArgs& a, int b, int 
   int iy, ix;
   if (a.transposed) {
     const int ty = oy + a.pad_y - ky, tx = ox + a.pad_x - kx;
-    if (ty < 0 || tx < 0 || ty % a.stride || tx % a.stride) return -1;
-    iy = ty / a.stride;
-    ix = tx / a.stride;
+    if (ty < 0 || tx < 0) return -1;
+    if (a.stride == 1) {  // (uniform branches: no integer division for the strides in use)
+      iy = ty;
+      ix = tx;
+    } else if (a.stride == 2) {
+      if ((ty | tx) & 1) return -1;
+      iy = ty >> 1;
+      ix = tx >> 1;
+    } else {
+      if (ty % a.stride || tx % a.stride) return -1;
+      iy = ty / a.stride;
+      ix = tx / a.stride;
+    }
   } else {
     iy = a.stride * oy + ky - a.pad_y;
     ix = a.stride * ox + kx - a.pad_x;
@@ -338,23 +348,46 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const long long per = (long long)a.uh * a.uw;
 
   f32x4 gv[GE], dv[DE];
+  // pixel coordinates (b, uy, ux) of each gat item's first u, advanced by TK per chunk with
+  // compares instead of the per-element integer divisions they replace
+  int ib_[GE], iy_[GE], ix_[GE];
+#pragma unroll
+  for (int e = 0; e < GE; ++e) {
+    const long long u = u0 + 4 * ((tid + 256 * e) / NA);
+    ib_[e] = (int)(u / per);
+    const int r = (int)(u - (long long)ib_[e] * per);
+    iy_[e] = r / a.uw;
+    ix_[e] = r - iy_[e] * a.uw;
+  }
+  auto step_pix = [&](int& b, int& y, int& x, int d) {
+    x += d;
+    while (x >= a.uw) {
+      x -= a.uw;
+      if (++y == a.uh) {
+        y = 0;
+        ++b;
+      }
+    }
+  };
   auto load = [&](long long ub) {
 #pragma unroll
     for (int e = 0; e < GE; ++e) {
       const int idx = tid + 256 * e, ug = idx / NA, row = r0 + idx % NA;
       const int tap = row / a.ca, ch = row - tap * a.ca, ky = tap / a.kw, kx = tap - ky * a.kw;
+      int b = ib_[e], uy = iy_[e], ux = ix_[e];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const long long u = ub + 4 * ug + i;
+        if (i) step_pix(b, uy, ux, 1);
         float v = 0.f;
         if (idx < TK / 4 * NA && row < a.rows && u < u1) {
-          const int b = (int)(u / per), r = (int)(u - (long long)b * per), uy = r / a.uw, ux = r - uy * a.uw;
-          const int iy = a.stride * uy + ky - a.pad_y, ix = a.stride * ux + kx - a.pad_x;
-          if ((unsigned)iy < (unsigned)a.gh && (unsigned)ix < (unsigned)a.gw)
-            v = a.gat[(((size_t)b * a.gh + iy) * a.gw + ix) * a.ca + ch];
+          const int gy = a.stride * uy + ky - a.pad_y, gx = a.stride * ux + kx - a.pad_x;
+          if ((unsigned)gy < (unsigned)a.gh && (unsigned)gx < (unsigned)a.gw)
+            v = a.gat[(((size_t)b * a.gh + gy) * a.gw + gx) * a.ca + ch];
         }
         gv[e][i] = v;
       }
+      step_pix(ib_[e], iy_[e], ix_[e], TK);  // this item's first u in the next chunk
     }
 #pragma unroll
     for (int e = 0; e < DE; ++e) {
