@@ -1298,17 +1298,40 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     hp.init(wave, lane, a.W);
   else
     hp.init(wave, lane);
-  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
-    const int t = bi + i * nb;
-    const int pl = t / per_plane;
-    p = p0 + pl;
-    const int r = t - pl * per_plane, ty = r / a.tiles_x;
-    t0y = ty * TH;
-    t0x = (r - ty * a.tiles_x) * TW;
+  // tile coordinates of the block's tiles bi, bi + nb, ... walked incrementally (the issue
+  // and epilogue sequences each visit them in order): no integer division per tile
+  const int d_pl = nb / per_plane, d_r = nb - d_pl * per_plane, d_ty = d_r / a.tiles_x, d_tx = d_r - d_ty * a.tiles_x;
+  struct TileIt {
+    int pl, ty, tx;
   };
-  auto issue = [&](int i) {
+  auto tile_first = [&]() {
+    TileIt s;
+    s.pl = bi / per_plane;
+    const int r = bi - s.pl * per_plane;
+    s.ty = r / a.tiles_x;
+    s.tx = r - s.ty * a.tiles_x;
+    return s;
+  };
+  auto tile_take = [&](TileIt& s, int& p, int& t0y, int& t0x) {  // coordinates of s, then s -> next tile
+    p = p0 + s.pl;
+    t0y = s.ty * TH;
+    t0x = s.tx * TW;
+    s.tx += d_tx;
+    if (s.tx >= a.tiles_x) {
+      s.tx -= a.tiles_x;
+      ++s.ty;
+    }
+    s.ty += d_ty;
+    if (s.ty >= a.tiles_y) {
+      s.ty -= a.tiles_y;
+      ++s.pl;
+    }
+    s.pl += d_pl;
+  };
+  TileIt it_issue = tile_first(), it_ep = tile_first();
+  auto issue = [&](int i) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
+    tile_take(it_issue, p, t0y, t0x);
     if constexpr (kBufHalo)
       hp.issue(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * plane_bytes, plane_bytes, a.W,
                t0y - a.pad_y, t0x - a.pad_x, wave);
@@ -1443,7 +1466,7 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         proj_store(proj_dst());
       }
     if (i == ntile) break;
-    tile_at(i, ep_p, ep_y, ep_x);
+    tile_take(it_ep, ep_p, ep_y, ep_x);
     if constexpr (RESID) {  // consumed by this tile's epilogue, after the next vmcnt(0)
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
