@@ -1197,6 +1197,43 @@ __device__ __forceinline__ void unswap16(const u32x4& q, f16x4& hi, f16x4& lo) {
 // 8-pixel rows); every ds_read_b128 16-lane group ({0-3, 12-15, 20-27}, ...) then hits 16
 // distinct slots for every tap shift (exhaustive search over x-linear / XOR swizzles), and
 // the image is whole 1-KB DMA pieces with no pad slots (25 instead of 32 for 10 x 10).
+// Tile coordinates of a persistent block's tiles bi, bi + nb, bi + 2 nb, ... of a plane
+// group (per_plane = tiles_y x tiles_x tiles per plane), walked in order without an integer
+// division per tile (each call sequence -- DMA issue, conv1, epilogue -- keeps its own walk).
+struct TileWalk {
+  int pl, ty, tx, d_pl, d_ty, d_tx, tiles_x, tiles_y;
+  __device__ __forceinline__ void init(int bi, int nb, int tiles_y_, int tiles_x_) {
+    tiles_x = tiles_x_;
+    tiles_y = tiles_y_;
+    const int per_plane = tiles_y * tiles_x;
+    pl = bi / per_plane;
+    const int r = bi - pl * per_plane;
+    ty = r / tiles_x;
+    tx = r - ty * tiles_x;
+    d_pl = nb / per_plane;
+    const int dr = nb - d_pl * per_plane;
+    d_ty = dr / tiles_x;
+    d_tx = dr - d_ty * tiles_x;
+  }
+  // plane index (within the group), tile row, tile column of the current tile; then advance
+  __device__ __forceinline__ void take(int& pl_, int& ty_, int& tx_) {
+    pl_ = pl;
+    ty_ = ty;
+    tx_ = tx;
+    tx += d_tx;
+    if (tx >= tiles_x) {
+      tx -= tiles_x;
+      ++ty;
+    }
+    ty += d_ty;
+    if (ty >= tiles_y) {
+      ty -= tiles_y;
+      ++pl;
+    }
+    pl += d_pl;
+  }
+};
+
 template <int CIN, int TH, int TW>
 struct GeomWS {
   static_assert(CIN == 64, "record geometry searched for Cin 64");
@@ -1298,37 +1335,16 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     hp.init(wave, lane, a.W);
   else
     hp.init(wave, lane);
-  // tile coordinates of the block's tiles bi, bi + nb, ... walked incrementally (the issue
-  // and epilogue sequences each visit them in order): no integer division per tile
-  const int d_pl = nb / per_plane, d_r = nb - d_pl * per_plane, d_ty = d_r / a.tiles_x, d_tx = d_r - d_ty * a.tiles_x;
-  struct TileIt {
+  TileWalk it_issue, it_ep;  // the DMA issue and the epilogue each visit the tiles in order
+  it_issue.init(bi, nb, a.tiles_y, a.tiles_x);
+  it_ep = it_issue;
+  auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
     int pl, ty, tx;
+    w.take(pl, ty, tx);
+    p = p0 + pl;
+    t0y = ty * TH;
+    t0x = tx * TW;
   };
-  auto tile_first = [&]() {
-    TileIt s;
-    s.pl = bi / per_plane;
-    const int r = bi - s.pl * per_plane;
-    s.ty = r / a.tiles_x;
-    s.tx = r - s.ty * a.tiles_x;
-    return s;
-  };
-  auto tile_take = [&](TileIt& s, int& p, int& t0y, int& t0x) {  // coordinates of s, then s -> next tile
-    p = p0 + s.pl;
-    t0y = s.ty * TH;
-    t0x = s.tx * TW;
-    s.tx += d_tx;
-    if (s.tx >= a.tiles_x) {
-      s.tx -= a.tiles_x;
-      ++s.ty;
-    }
-    s.ty += d_ty;
-    if (s.ty >= a.tiles_y) {
-      s.ty -= a.tiles_y;
-      ++s.pl;
-    }
-    s.pl += d_pl;
-  };
-  TileIt it_issue = tile_first(), it_ep = tile_first();
   auto issue = [&](int i) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
     tile_take(it_issue, p, t0y, t0x);
@@ -1620,33 +1636,48 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   int boff[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
-  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
-    const int t = bi + i * nb;
-    const int pl = t / per_plane;
+  // tiles walked in order by each call sequence (DMA issue, epilogue, FUSE1 RGB loads)
+  TileWalk w_issue, w_ep, w_rgb;
+  w_issue.init(bi, nb, a.tiles_y, a.tiles_x);
+  w_ep = w_rgb = w_issue;
+  auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
+    int pl, ty, tx;
+    w.take(pl, ty, tx);
     p = p0 + pl;
-    const int r = t - pl * per_plane, ty = r / a.tiles_x;
     t0y = ty * TH;
-    t0x = (r - ty * a.tiles_x) * TW;
+    t0x = tx * TW;
   };
-  // this wave's DMA pieces of a halo: slot q -> (row, stored pixel sp, slot k)
-  auto issue = [&](int i) {
+  // this wave's DMA pieces of a halo: slot q -> (row, stored pixel sp, slot k), resolved once:
+  // per piece the byte offset from the halo origin pixel and (row << 8 | column) for the
+  // image-bounds test (kDmaOOR: pad slot, the buffer DMA writes zeros)
+  unsigned doff[NPP];
+  int drc[NPP];
+#pragma unroll
+  for (int j = 0; j < NPP; ++j) {
+    const int piece = wave + j * NW;
+    const int q = piece * 64 + lane;
+    const int row = q / G::RPS, r = q - row * G::RPS;
+    const int sp = r / G::PSS, k = r - sp * G::PSS;
+    const int hx = sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1;
+    const bool ok = piece < G::NPIECE && q < G::HTOT && sp < G::HW && k < CIN / 4;
+    doff[j] = ok ? (unsigned)((row * a.W + hx) * CIN * 4 + k * 16) : kDmaOOR;
+    drc[j] = row << 8 | hx;
+  }
+  const unsigned plane_bytes = (unsigned)((size_t)a.H * a.W * CIN * 4);
+  auto issue = [&](int i) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
+    tile_take(w_issue, p, t0y, t0x);
     const int gy0 = 2 * t0y - a.pad_y, gx0 = 2 * t0x - a.pad_x;
-    const char* base = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+    const unsigned org = (unsigned)((gy0 * a.W + gx0) * CIN * 4);
     char* buf = lds + (i & 1) * G::HALO_BYTES;
 #pragma unroll
     for (int j = 0; j < NPP; ++j) {
       const int piece = wave + j * NW;
       if (NPP * NW > G::NPIECE && piece >= G::NPIECE) break;  // wave-uniform
-      const int q = piece * 64 + lane;
-      const int row = q / G::RPS, r = q - row * G::RPS;
-      const int sp = r / G::PSS, k = r - sp * G::PSS;
-      const int hx = sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1;
-      const int gy = gy0 + row, gx = gx0 + hx;
-      const bool ok = q < G::HTOT && sp < G::HW && k < CIN / 4 && (unsigned)gy < (unsigned)a.H &&
-                      (unsigned)gx < (unsigned)a.W;
-      dma16(ok ? base + ((size_t)(unsigned)(gy * a.W + gx) * CIN * 4 + k * 16) : a.zero16, buf + piece * 1024);
+      const bool in = (unsigned)(gy0 + (drc[j] >> 8)) < (unsigned)a.H && (unsigned)(gx0 + (drc[j] & 255)) < (unsigned)a.W;
+      dma16_buf(rsrc, doff[j] != kDmaOOR && in ? doff[j] + org : kDmaOOR, buf + piece * 1024);
     }
   };
 
@@ -1662,9 +1693,9 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int tid1 = (int)threadIdx.x - 256;
   int pl_type = 0;  // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
   // plain loads, unpacked only by the next tile's patch phase (no wait before the MFMAs)
-  auto rgb_load = [&](int i) {
+  auto rgb_load = [&](int) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
+    tile_take(w_rgb, p, t0y, t0x);
     const int n = p % a.nimg;
     pl_type = p / a.nimg;
     const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
@@ -1772,7 +1803,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     if constexpr (!FUSE1) {
       if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
     }
-    tile_at(i, ep_p, ep_y, ep_x);
+    tile_take(w_ep, ep_p, ep_y, ep_x);
     const char* buf = lds + (FUSE1 ? 0 : (i & 1)) * G::HALO_BYTES;
     if constexpr (FUSE1) {
       // colour plane of the patch (utils.py:74-77: x/255, ((r k0 + g k1) + b k2) + off, every op
@@ -2017,14 +2048,18 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   int boff[MT];  // B fragment of pixel tile m at tap (0, 0): halo row 2 (2m + l16/8), column l16 % 8
 #pragma unroll
   for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
-  auto tile_at = [&](int i, int& p, int& t0y, int& t0x) {
-    const int t = bi + i * nb;
-    const int pl = t / per_plane;
+  // tiles walked in order by each call sequence (patch DMA, conv1, epilogue)
+  TileWalk w_patch, w_c1, w_ep;
+  w_patch.init(bi, nb, a.tiles_y, a.tiles_x);
+  w_c1 = w_ep = w_patch;
+  auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
+    int pl, ty, tx;
+    w.take(pl, ty, tx);
     p = p0 + pl;
-    const int r = t - pl * per_plane, ty = r / a.tiles_x;
     t0y = ty * TH;
-    t0x = (r - ty * a.tiles_x) * TW;
+    t0x = tx * TW;
   };
+
 
   // conv1 A fragments / bias / scale and this lane's im2col tap-pair offsets in a patch
   // plane (bytes; pair = kh * 3 + kw / 2; pad pairs >= 15 read any finite element: their
@@ -2062,7 +2097,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   const size_t cp_plane = (size_t)a.cp_h * a.cp_w;  // f16 elements per colour plane
   auto patch_dma = [&](int i) {  // tile i's patch into patch buffer i & 1
     int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
+    tile_take(w_patch, p, t0y, t0x);  // patch_dma is called for i = 0, 1, 2, ... in order
     const unsigned org = (unsigned)((4 * t0y * a.cp_w + 4 * t0x) * 2);
     char* dst = patches + (i & 1) * 2 * C12_PLANE;
 #pragma unroll
@@ -2086,7 +2121,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     constexpr int PTW = TS == 0 ? PT0 : PT1, PTB = TS == 0 ? 0 : 4 * PT0;
     if constexpr (PTW > 0) {
       int p, t0y, t0x;
-      tile_at(i, p, t0y, t0x);
+      tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
       char* halo = lds + (i & 1) * G::HALO_BYTES;
       const char* ph = patches + (i & 1) * 2 * C12_PLANE;
       const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;  // halo origin, conv1-output coords
@@ -2179,7 +2214,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
   auto epilogue = [&](int i) {  // ts 0: own sums + the ts 1 partials, bias, leaky, split, 16-B stores
     int p, t0y, t0x;
-    tile_at(i, p, t0y, t0x);
+    tile_take(w_ep, p, t0y, t0x);  // epilogue is called for i = 0, 1, 2, ... in order
     const char* pp = part + cg * PART + lane * 16;
     f32x4 q4[MT];  // all partial reads in flight before the first use
 #pragma unroll
