@@ -83,6 +83,15 @@ __device__ unsigned long long* g_stamps;
   } while (0)
 #endif
 
+// b / 255 for a byte b, correctly rounded like the host table c_u8_to_unit (NumPy's
+// x.astype(f32) / 255), in registers: r = b * fl(1/255), then one FMA correction step.  Exact
+// for every b in 0..255 (checked against exact rationals: tests/test_oracle.py).
+__device__ __forceinline__ float u8_unit(unsigned b) {
+  const float f = (float)b, c = 0.0039215688593685627f;  // fl(1/255)
+  const float r = __fmul_rn(f, c);
+  return __builtin_fmaf(__builtin_fmaf(-r, 255.0f, f), c, r);
+}
+
 __device__ __forceinline__ float leaky02(float z) {
   // tf.nn.leaky_relu(z, alpha=0.2) = max(alpha*z, z)
   return fmaxf(__fmul_rn(z, 0.2f), z);
@@ -673,10 +682,10 @@ __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int 
         v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * CIN + c4 * 4);
       } else {
         const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
-        v[b][0] = c_u8_to_unit[q & 255];
-        v[b][1] = c_u8_to_unit[(q >> 8) & 255];
-        v[b][2] = c_u8_to_unit[(q >> 16) & 255];
-        v[b][3] = c_u8_to_unit[q >> 24];
+        v[b][0] = u8_unit(q & 255);  // in registers: no table load per byte
+        v[b][1] = u8_unit((q >> 8) & 255);
+        v[b][2] = u8_unit((q >> 16) & 255);
+        v[b][3] = u8_unit(q >> 24);
       }
     }
 #pragma unroll
@@ -1996,7 +2005,7 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
       const int x = 2 * c2 + e - ox;
       const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
       const uint8_t* px = rgb + (((size_t)n * H + (in ? y : 0)) * W + (in ? x : 0)) * 3;
-      const float r8 = c_u8_to_unit[px[0]], g8 = c_u8_to_unit[px[1]], b8 = c_u8_to_unit[px[2]];
+      const float r8 = u8_unit(px[0]), g8 = u8_unit(px[1]), b8 = u8_unit(px[2]);
 #pragma unroll
       for (int k = 0; k < 3; ++k) v[k][e] = in ? __fadd_rn(project(c_ycbcr + 3 * k, r8, g8, b8), c_ycbcr_off[k]) : 0.f;
     }

@@ -200,3 +200,23 @@ def test_tile_patches_roundtrip():
     np.testing.assert_array_equal(untile_patches(t, 2, 512, 768), x)
     with pytest.raises(ValueError):
         tile_patches(x[:, :300], 256)
+
+
+def test_u8_unit_register_division_is_correctly_rounded():
+    # csrc u8_unit: b / 255 as r = b * fl(1/255), r += fma(-r, 255, b) * fl(1/255) in fp32 --
+    # equal to the correctly rounded b / 255 (the device table c_u8_to_unit, NumPy's
+    # astype(f32) / 255) for every byte; exact rational arithmetic for each rounding step
+    from fractions import Fraction as F
+
+    def r32(x):
+        c = np.float32(float(x))
+        cands = [np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))]
+        return min(cands, key=lambda v: (abs(F(float(v)) - x), int(np.float32(v).view(np.uint32)) & 1))
+
+    c = np.float32(0.0039215688593685627)
+    assert c == r32(F(1, 255))
+    for b in range(256):
+        r = r32(F(b) * F(float(c)))
+        e = r32(F(b) - F(float(r)) * 255)
+        q = r32(F(float(e)) * F(float(c)) + F(float(r)))
+        assert q == np.float32(b) / np.float32(255), b
