@@ -2691,27 +2691,41 @@ __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
   const int mx = (tb - tyi * a.tiles_x) * 16 + 2 * (lane & 7) + (wave & 1);
   if (my >= a.H || mx >= a.W) return;
   constexpr int TB[4] = {0, 4, 10, 16};  // phase-major tap bases (for_each_phase_tap)
+  // the 9 neighbours' tap-0 byte offsets inside one plane's projection block (the same for
+  // the three planes), resolved once; neighbours outside the image get an offset past the
+  // buffer, whose loads return 0.  Buffer loads from a per-plane resource keep every address
+  // 32-bit and the tap offsets in the instruction's immediate.
+  const unsigned plane_floats = 4u * a.tiles_y7 * a.tiles_x7 * (25u * 64u);
+  unsigned off[3][3];
+#pragma unroll
+  for (int iy = 0; iy < 3; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < 3; ++ix) {
+      const int ny = my - 1 + iy, nx = mx - 1 + ix;
+      const bool ok = (unsigned)ny < (unsigned)a.H && (unsigned)nx < (unsigned)a.W;
+      const int cy = ny >> 1, cx = nx >> 1, ph7 = (ny & 1) * 2 + (nx & 1);
+      off[iy][ix] = ok ? (((unsigned)((ph7 * a.tiles_y7 + (cy >> 3)) * a.tiles_x7 + (cx >> 3)) * (25u * 64u) +
+                           (unsigned)((cy & 7) * 8 + (cx & 7))) * 4u)
+                       : kDmaOOR;
+    }
   float outv[3][4];
 #pragma unroll
   for (int type = 0; type < 3; ++type) {
     const int p = type * a.nimg + n;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.proj + (size_t)p * plane_floats), (short)0, (int)(plane_floats * 4u), kBufWord3);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int iy = 0; iy < 3; ++iy)
 #pragma unroll
       for (int ix = 0; ix < 3; ++ix) {
-        const int ny = my - 1 + iy, nx = mx - 1 + ix;
-        const bool ok = (unsigned)ny < (unsigned)a.H && (unsigned)nx < (unsigned)a.W;
-        const int cy = ok ? ny >> 1 : 0, cx = ok ? nx >> 1 : 0, ph7 = ok ? (ny & 1) * 2 + (nx & 1) : 0;
-        const float* src =
-            a.proj + ((((size_t)p * 4 + ph7) * a.tiles_y7 + (cy >> 3)) * a.tiles_x7 + (cx >> 3)) * (25 * 64) +
-            (cy & 7) * 8 + (cx & 7);
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph) {
           const int py = ph >> 1, px = ph & 1;
           if (iy < 2 + py && ix < 2 + px) {
-            const float v = src[(TB[ph] + iy * (2 + px) + ix) * 64];
-            acc[ph] = __fadd_rn(acc[ph], ok ? v : 0.f);
+            const float v = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rs, off[iy][ix] + (TB[ph] + iy * (2 + px) + ix) * 256, 0, 0));
+            acc[ph] = __fadd_rn(acc[ph], v);
           }
         }
       }
