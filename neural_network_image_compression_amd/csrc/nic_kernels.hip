@@ -1373,6 +1373,18 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   // 16-B output granule of this lane after swap16_pair: [hi | lo] half (g & 1), channels
   // 16w + 8 (g >> 1) .. +7
   const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
+  // output / residual granules through per-plane buffer resources: per lane and pixel tile m
+  // the byte offset of its granule from the tile origin's, resolved once (32-bit; a granule
+  // outside the image gets kDmaOOR: the store is dropped, the residual DMA writes zeros)
+  constexpr int PXB = COUT * 4;  // bytes per split pixel record
+  const unsigned out_plane = (unsigned)((size_t)a.OH * a.OW * PXB);
+  unsigned g_off[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int dy = 2 * m + (l16 >> 3), dx = l16 & 7;
+    g_off[m] = TRP ? (unsigned)(((2 * dy) * a.OW + 2 * dx) * PXB + st_off * 2)
+                   : (unsigned)((dy * a.OW + dx) * PXB + st_off * 2);
+  }
   int ep_p = 0, ep_y = 0, ep_x = 0;  // tile whose epilogue is pending
   float rmax = 0.f;                  // range guard of the split output
   // PROJ: tile i-1's projection, 4 chunks (tap block nt, k32-step ks) of 3 MFMAs, runs
@@ -1433,6 +1445,14 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     s_wait += s_t1 - s_t0;
 #endif
     if (i > 0) {  // epilogue of tile i-1: *2^-k, bias, leaky (+ residual), split, 8-B stores
+      __amdgpu_buffer_rsrc_t out_rs;
+      unsigned out_org = 0;
+      if constexpr (!PROJ) {
+        out_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.out_s + (size_t)ep_p * out_plane / 2), (short)0,
+                                                   (int)out_plane, kBufWord3);
+        out_org = TRP ? (unsigned)(((2 * ep_y + py) * a.OW + 2 * ep_x + px) * PXB)
+                      : (unsigned)((ep_y * a.OW + ep_x) * PXB);
+      }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
@@ -1461,9 +1481,8 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         if constexpr (PROJ) {  // chunk (g & 1) * 8 + 2w + g / 2 of pixel 16m + l16
           const int pp = 16 * m + l16, ch = (g & 1) * 8 + 2 * wave + (g >> 1);
           *(u32x4*)(hproj + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
-        } else if (y < a.H && x < a.W) {
-          const int oy = TRP ? 2 * y + py : y, ox = TRP ? 2 * x + px : x;
-          *(u32x4*)(a.out_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = q;
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(q, out_rs, y < a.H && x < a.W ? out_org + g_off[m] : kDmaOOR, 0, 0);
         }
       }
     }
@@ -1493,14 +1512,21 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     if (i == ntile) break;
     tile_take(it_ep, ep_p, ep_y, ep_x);
     if constexpr (RESID) {  // consumed by this tile's epilogue, after the next vmcnt(0)
+      if constexpr (kResDma) {  // this wave's own LDS region: its reads came first
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.res_s + (size_t)ep_p * out_plane / 2), (short)0, (int)out_plane, kBufWord3);
+        const unsigned org = (unsigned)((ep_y * a.OW + ep_x) * PXB);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int oy = min(ep_y + 2 * m + (l16 >> 3), a.OH - 1), ox = min(ep_x + (l16 & 7), a.OW - 1);
-        const uint16_t* src = a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off;
-        if constexpr (kResDma)
-          dma16((const char*)src, res_lds + m * 1024);  // this wave's own region: its reads came first
-        else
-          rq[m] = *(const u32x4*)src;
+        for (int m = 0; m < MT; ++m) {
+          const bool in = ep_y + 2 * m + (l16 >> 3) < a.OH && ep_x + (l16 & 7) < a.OW;
+          dma16_buf(rs, in ? org + g_off[m] : kDmaOOR, res_lds + m * 1024);
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int oy = min(ep_y + 2 * m + (l16 >> 3), a.OH - 1), ox = min(ep_x + (l16 & 7), a.OW - 1);
+          rq[m] = *(const u32x4*)(a.res_s + (((size_t)ep_p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off);
+        }
       }
     }
     const char* buf = lds + (i & 1) * G::HALO_BYTES;
