@@ -3153,11 +3153,11 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
 // block writes its 3 x 256 partial counts (no atomics, no memset); hist_entropy_kernel
 // reduces them.  HBM-bound: 1 B read per code.
 constexpr int HIST_UNR = 4;  // 16-B loads in flight per thread
-template <int R, bool ZB>
-__global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restrict__ z, int nimg, int plane_px,
+template <int R, bool ZB, int NT>
+__global__ __launch_bounds__(NT) void latent_hist_kernel(const uint8_t* __restrict__ z, int nimg, int plane_px,
                                                           uint32_t* __restrict__ counts, int chunk_vec) {
   __shared__ uint32_t h[3 * 256 * R];
-  for (int i = threadIdx.x; i < 3 * 256 * R; i += 256) h[i] = 0;
+  for (int i = threadIdx.x; i < 3 * 256 * R; i += NT) h[i] = 0;
   __syncthreads();
   const int n = blockIdx.y;
   const int nvec = plane_px * 6;
@@ -3167,15 +3167,15 @@ __global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restr
   const int lane = threadIdx.x & 63;
   uint32_t* hr = h + (threadIdx.x & (R - 1));
   uint32_t zeros[3] = {0, 0, 0};  // ZB: per-lane count of code 0, per plane
-  for (int v = v0 + threadIdx.x; v < v1; v += 256 * HIST_UNR) {
+  for (int v = v0 + threadIdx.x; v < v1; v += NT * HIST_UNR) {
     u32x4 q[HIST_UNR];
 #pragma unroll
     for (int u = 0; u < HIST_UNR; ++u)
-      q[u] = v + u * 256 < v1 ? __builtin_nontemporal_load(base + v + u * 256) : u32x4{0, 0, 0, 0};
+      q[u] = v + u * NT < v1 ? __builtin_nontemporal_load(base + v + u * NT) : u32x4{0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < HIST_UNR; ++u) {
-      if (v + u * 256 >= v1) break;
-      const int plane = ((v + u * 256) % 6) >> 1;
+      if (v + u * NT >= v1) break;
+      const int plane = ((v + u * NT) % 6) >> 1;
       uint32_t* hp = hr + plane * (256 * R);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -3208,7 +3208,7 @@ __global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restr
   }
   __syncthreads();
   // partial counts of this block: part[type][n][chunk][bin] (reduced by hist_entropy_kernel)
-  for (int i = threadIdx.x; i < 3 * 256; i += 256) {
+  for (int i = threadIdx.x; i < 3 * 256; i += NT) {
     uint32_t c = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) c += h[i * R + r];
@@ -3219,28 +3219,33 @@ __global__ __launch_bounds__(256) void latent_hist_kernel(const uint8_t* __restr
 
 __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __restrict__ part, int chunks, float n_sym,
                                                             uint32_t* __restrict__ counts, float* __restrict__ bits) {
-  // one block per plane p; thread (g, bin) sums every 4th partial of the plane (exact
-  // integers, 8 loads in flight), the 4 groups meet in LDS.  Then p_i = c_i / N (fp32),
+  // one block per plane p; thread (g, q) sums bins 4q..4q+3 (one 16-B load) of every 16th
+  // partial of the plane (exact integers, 16 loads in flight: one round covers 256 partials),
+  // the 16 groups meet in LDS.  Then p_i = c_i / N (fp32),
   // term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2), summed in double.
-  __shared__ uint32_t grp[3][256];
+  __shared__ u32x4 grp[16][64];
   __shared__ double red[4];
   const int p = blockIdx.x;
-  const int bin = threadIdx.x & 255, g = threadIdx.x >> 8;
-  const uint32_t* src = part + (size_t)p * chunks * 256 + bin;
-  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int k0 = g; k0 < chunks; k0 += 64) {  // 16 predicated loads in flight per round
+  const int q = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const u32x4* src = (const u32x4*)(part + (size_t)p * chunks * 256) + q;
+  u32x4 acc[4] = {};
+  for (int k0 = g; k0 < chunks; k0 += 256) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int k = k0 + 4 * u;
-      acc[u & 7] += k < chunks ? src[(size_t)k * 256] : 0u;
+      const int k = k0 + 16 * u;
+      acc[u & 3] += k < chunks ? src[(size_t)k * 64] : u32x4{0, 0, 0, 0};
     }
   }
-  uint32_t c = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  if (g) grp[g - 1][bin] = c;
+  grp[g][q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
+  const int bin = threadIdx.x;
+  uint32_t c = 0;
+  if (bin < 256) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c += ((const uint32_t*)grp[j])[bin];
+  }
   double s = 0.0;
-  if (g == 0) {
-    c += grp[0][bin] + grp[1][bin] + grp[2][bin];
+  if (bin < 256) {
     if (counts) counts[(size_t)p * 256 + bin] = c;
     const float pr = __fdiv_rn((float)c, n_sym);
     const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
@@ -3749,36 +3754,43 @@ hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
-int hist_chunks(int nimg, int plane_px, int* chunk_vec) {
-  // ~1536 blocks over the whole batch (6 resident per CU x 256 CUs: one full wave of
-  // blocks, no tail round), 4 KB .. 256 KB of latent each
+int hist_chunks(int nimg, int plane_px, int* chunk_vec, int blocks) {
+  // `blocks` over the whole batch (one full wave of blocks, no tail round: 6 resident
+  // 256-thread blocks or 2 1024-thread blocks per CU x 256 CUs), 4 KB .. 256 KB of latent each
   const long long nvec = (long long)plane_px * 6;
-  long long cv = ((nvec * nimg + 1535) / 1536 + 255) / 256 * 256;
+  long long cv = ((nvec * nimg + blocks - 1) / blocks + 255) / 256 * 256;
   cv = cv < 256 ? 256 : (cv > 16384 ? 16384 : cv);
   *chunk_vec = (int)cv;
   return (int)((nvec + cv - 1) / cv);
 }
 
 size_t hist_scratch_bytes(int nimg, int plane_px) {
-  int cv;
-  return (size_t)3 * nimg * hist_chunks(nimg, plane_px, &cv) * 256 * sizeof(uint32_t);
+  int cv;  // sized for the most partials any variant writes
+  return (size_t)3 * nimg * hist_chunks(nimg, plane_px, &cv, 1536) * 256 * sizeof(uint32_t);
 }
 
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
                        hipStream_t st) {
-  int chunk_vec;
-  const int chunks = hist_chunks(nimg, plane_px, &chunk_vec);
   const char* hv = getenv("NIC_HIST");
-  // A/B switch (tools/hist_ab.py): 8 replicas measured best (a packed-u16 32-replica
-  // layout, conflict-free by construction, was 15 % slower)
+  // Default: 1024-thread blocks, 512 of them (2 per CU) from 24 MB of latent up, else 256
+  // (>= 48 KB per block: the per-block LDS clear and 768 partial stores amortised).
+  // A/B switch (tools/hist_ab.py): NIC_HIST=<R>[z] = 256-thread blocks with R replicas
+  // (1536 blocks; 8 replicas measured best, a packed-u16 32-replica layout was 15 % slower),
+  // <R>b<N> = 1024-thread blocks, N x 256 of them.
+  const bool big = !hv || hv[1] == 'b';
   const char m = hv ? hv[0] : '8';
   const bool zb = hv && hv[1] == 'z';
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(256), 0, st, z, nimg, plane_px, part, chunk_vec);
+  const long long total = (long long)plane_px * 96 * nimg;
+  const int bmul = hv && big && hv[2] >= '1' && hv[2] <= '6' ? hv[2] - '0' : (total >= (24ll << 20) ? 2 : 1);
+  int chunk_vec;
+  const int chunks = hist_chunks(nimg, plane_px, &chunk_vec, big ? 256 * bmul : 1536);
+  auto go = [&](auto kern, int nt) {
+    hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(nt), 0, st, z, nimg, plane_px, part, chunk_vec);
   };
-  if (m == '1') zb ? go(latent_hist_kernel<1, true>) : go(latent_hist_kernel<1, false>);
-  else if (m == '8') zb ? go(latent_hist_kernel<8, true>) : go(latent_hist_kernel<8, false>);
-  else zb ? go(latent_hist_kernel<4, true>) : go(latent_hist_kernel<4, false>);
+  if (big) m == '4' ? go(latent_hist_kernel<4, false, 1024>, 1024) : go(latent_hist_kernel<8, false, 1024>, 1024);
+  else if (m == '1') zb ? go(latent_hist_kernel<1, true, 256>, 256) : go(latent_hist_kernel<1, false, 256>, 256);
+  else if (m == '8') zb ? go(latent_hist_kernel<8, true, 256>, 256) : go(latent_hist_kernel<8, false, 256>, 256);
+  else zb ? go(latent_hist_kernel<4, true, 256>, 256) : go(latent_hist_kernel<4, false, 256>, 256);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, chunks, (float)plane_px * 32.0f,

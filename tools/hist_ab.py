@@ -1,6 +1,6 @@
-"""A/B of the histogram-entropy kernel variants (NIC_HIST=<replicas><z?>) on real 4K latents.
+"""A/B of the histogram-entropy kernel variants (NIC_HIST, see launch_hist) on real 4K latents.
 
-    python tools/hist_ab.py [frames]
+    python tools/hist_ab.py [frames] [variants, comma-separated; d = library default]
 """
 import os
 import sys
@@ -21,8 +21,11 @@ x = torch.randint(0, 256, (F, 2160, 3840, 3), generator=g, dtype=torch.uint8).cu
 z = c.encode(x)
 torch.cuda.synchronize()
 ref = None
-for v in ["1", "4", "8", "8z"]:
-    os.environ["NIC_HIST"] = v
+for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "4", "8", "8z"]):
+    if v == "d":  # the library default
+        os.environ.pop("NIC_HIST", None)
+    else:
+        os.environ["NIC_HIST"] = v
     for _ in range(3):
         bits, cnt = c.entropy(z, counts=True)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
