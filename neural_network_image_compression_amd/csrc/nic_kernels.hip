@@ -2015,34 +2015,33 @@ void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int*
 
 // One thread per (image, padded row, column pair): the three colour planes of two pixels,
 // split into hi / lo f16 (zero outside the image), one dword store per plane and half.
+// Grid (ceil(hp * wp / 2 / 256), N): the image is blockIdx.y, the rest 32-bit index math.
 __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __restrict__ rgb, uint16_t* __restrict__ cp,
                                                            int N, int H, int W, int oy, int ox, int hp, int wp) {
   const int pairs = wp / 2;
-  const long long total = (long long)N * hp * pairs;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= hp * pairs) return;
+  const int n = blockIdx.y;
+  const int yp = t / pairs, c2 = t - yp * pairs;
   const size_t plane = (size_t)hp * wp, P = 3 * (size_t)N;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int c2 = (int)(t % pairs);
-    const long long r = t / pairs;
-    const int yp = (int)(r % hp), n = (int)(r / hp);
-    const int y = yp - oy;
-    float v[3][2];
+  const int y = yp - oy;
+  float v[3][2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int x = 2 * c2 + e - ox;
-      const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      const uint8_t* px = rgb + (((size_t)n * H + (in ? y : 0)) * W + (in ? x : 0)) * 3;
-      const float r8 = u8_unit(px[0]), g8 = u8_unit(px[1]), b8 = u8_unit(px[2]);
+  for (int e = 0; e < 2; ++e) {
+    const int x = 2 * c2 + e - ox;
+    const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const uint8_t* px = rgb + (((size_t)n * H + (in ? y : 0)) * W + (in ? x : 0)) * 3;
+    const float r8 = u8_unit(px[0]), g8 = u8_unit(px[1]), b8 = u8_unit(px[2]);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) v[k][e] = in ? __fadd_rn(project(c_ycbcr + 3 * k, r8, g8, b8), c_ycbcr_off[k]) : 0.f;
-    }
+    for (int k = 0; k < 3; ++k) v[k][e] = in ? __fadd_rn(project(c_ycbcr + 3 * k, r8, g8, b8), c_ycbcr_off[k]) : 0.f;
+  }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const _Float16 h0 = (_Float16)v[k][0], h1 = (_Float16)v[k][1];
-      const _Float16 l0 = (_Float16)(v[k][0] - (float)h0), l1 = (_Float16)(v[k][1] - (float)h1);
-      const size_t o = ((size_t)k * N + n) * plane + (size_t)yp * wp + 2 * c2;  // plane k N + n
-      *(uint32_t*)(cp + o) = (uint32_t)__builtin_bit_cast(uint16_t, h0) | (uint32_t)__builtin_bit_cast(uint16_t, h1) << 16;
-      *(uint32_t*)(cp + P * plane + o) = (uint32_t)__builtin_bit_cast(uint16_t, l0) | (uint32_t)__builtin_bit_cast(uint16_t, l1) << 16;
-    }
+  for (int k = 0; k < 3; ++k) {
+    const _Float16 h0 = (_Float16)v[k][0], h1 = (_Float16)v[k][1];
+    const _Float16 l0 = (_Float16)(v[k][0] - (float)h0), l1 = (_Float16)(v[k][1] - (float)h1);
+    const size_t o = ((size_t)k * N + n) * plane + (size_t)t * 2;  // plane k N + n, element 2 t
+    *(uint32_t*)(cp + o) = (uint32_t)__builtin_bit_cast(uint16_t, h0) | (uint32_t)__builtin_bit_cast(uint16_t, h1) << 16;
+    *(uint32_t*)(cp + P * plane + o) = (uint32_t)__builtin_bit_cast(uint16_t, l0) | (uint32_t)__builtin_bit_cast(uint16_t, l1) << 16;
   }
 }
 
@@ -3628,11 +3627,11 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
   c12_plane_geom(a.OH, a.OW, a.pad_y, a.pad_x, a.p1y, a.p1x, &oy, &ox, &a.cp_h, &a.cp_w);
   // 32-bit byte offsets inside one plane (buffer resources of the patch DMA)
   if ((long long)a.cp_h * a.cp_w * 2 >= (1LL << 31)) return hipErrorInvalidValue;
-  const long long work = (long long)a.nimg * a.cp_h * (a.cp_w / 2);
-  if (work == 0) return hipSuccess;
-  const int blocks = (int)std::min<long long>((work + 255) / 256, 16LL * device_cus());
-  hipLaunchKernelGGL(colour_split_kernel, dim3(blocks), dim3(256), 0, st, a.rgb, a.cplane, a.nimg, a.H0, a.W0, oy, ox,
-                     a.cp_h, a.cp_w);
+  const long long per_img = (long long)a.cp_h * (a.cp_w / 2);  // < 2^31 (checked above)
+  if (per_img == 0 || a.nimg == 0) return hipSuccess;
+  if (a.nimg > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colour_split_kernel, dim3((unsigned)((per_img + 255) / 256), a.nimg), dim3(256), 0, st, a.rgb,
+                     a.cplane, a.nimg, a.H0, a.W0, oy, ox, a.cp_h, a.cp_w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
