@@ -3151,8 +3151,8 @@ __global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
 // so lanes that hit the same bin (skewed latents: ~40 % zeros) spread over R banks.  Each
 // block writes its 3 x 256 partial counts (no atomics, no memset); hist_entropy_kernel
 // reduces them.  HBM-bound: 1 B read per code.
-constexpr int HIST_UNR = 4;  // 16-B loads in flight per thread
-template <int R, bool ZB, int NT>
+constexpr int HIST_UNR_DEFAULT = 4;  // 16-B loads in flight per thread
+template <int R, bool ZB, int NT, int HIST_UNR = HIST_UNR_DEFAULT>
 __global__ __launch_bounds__(NT) void latent_hist_kernel(const uint8_t* __restrict__ z, int nimg, int plane_px,
                                                           uint32_t* __restrict__ counts, int chunk_vec) {
   __shared__ uint32_t h[3 * 256 * R];
@@ -3771,22 +3771,28 @@ size_t hist_scratch_bytes(int nimg, int plane_px) {
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
                        hipStream_t st) {
   const char* hv = getenv("NIC_HIST");
-  // Default: 1024-thread blocks, 512 of them (2 per CU) from 24 MB of latent up, else 256
-  // (>= 48 KB per block: the per-block LDS clear and 768 partial stores amortised).
+  // Default: 1024-thread blocks, 512 of them (2 per CU) with 16 LDS replicas per bin from
+  // 24 MB of latent up, else 256 with 8 (>= 48 KB per block: the per-block LDS clear and 768
+  // partial stores amortised).
   // A/B switch (tools/hist_ab.py): NIC_HIST=<R>[z] = 256-thread blocks with R replicas
   // (1536 blocks; 8 replicas measured best, a packed-u16 32-replica layout was 15 % slower),
-  // <R>b<N> = 1024-thread blocks, N x 256 of them.
+  // <R>b<N>[u] = 1024-thread blocks, N x 256 of them (R: 4, 8, g = 16, h = 32; u = 8 loads in
+  // flight).  4K x 8 latents: 16 replicas 21.6 us, 8: 25.4, 32 (98 KB, 1 block per CU): 27.2.
   const bool big = !hv || hv[1] == 'b';
-  const char m = hv ? hv[0] : '8';
-  const bool zb = hv && hv[1] == 'z';
   const long long total = (long long)plane_px * 96 * nimg;
+  const char m = hv ? hv[0] : (total >= (24ll << 20) ? 'g' : '8');
+  const bool zb = hv && hv[1] == 'z';
   const int bmul = hv && big && hv[2] >= '1' && hv[2] <= '6' ? hv[2] - '0' : (total >= (24ll << 20) ? 2 : 1);
   int chunk_vec;
   const int chunks = hist_chunks(nimg, plane_px, &chunk_vec, big ? 256 * bmul : 1536);
   auto go = [&](auto kern, int nt) {
     hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(nt), 0, st, z, nimg, plane_px, part, chunk_vec);
   };
-  if (big) m == '4' ? go(latent_hist_kernel<4, false, 1024>, 1024) : go(latent_hist_kernel<8, false, 1024>, 1024);
+  const bool u8x = big && hv && hv[2] && hv[3] == 'u';
+  if (big && m == 'h') go(latent_hist_kernel<32, false, 1024>, 1024);
+  else if (big && m == 'g') u8x ? go(latent_hist_kernel<16, false, 1024, 8>, 1024) : go(latent_hist_kernel<16, false, 1024>, 1024);
+  else if (big && m == '4') go(latent_hist_kernel<4, false, 1024>, 1024);
+  else if (big) u8x ? go(latent_hist_kernel<8, false, 1024, 8>, 1024) : go(latent_hist_kernel<8, false, 1024>, 1024);
   else if (m == '1') zb ? go(latent_hist_kernel<1, true, 256>, 256) : go(latent_hist_kernel<1, false, 256>, 256);
   else if (m == '8') zb ? go(latent_hist_kernel<8, true, 256>, 256) : go(latent_hist_kernel<8, false, 256>, 256);
   else zb ? go(latent_hist_kernel<4, true, 256>, 256) : go(latent_hist_kernel<4, false, 256>, 256);
