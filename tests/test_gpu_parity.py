@@ -277,6 +277,30 @@ def test_entropy_counter_capacity(codecs):
     del z
 
 
+@pytest.fixture(scope="module")
+def skewed_latent():
+    # two 4K-frame latents (24.9 MB: the large-latent default), ~40 % zeros like real latents
+    rng = np.random.default_rng(13)
+    z = rng.integers(0, 256, (2, 270, 480, 96), dtype=np.uint8)
+    z[rng.random(z.shape, dtype=np.float32) < 0.4] = 0
+    return z, O.histograms(z), O.hist_entropy(z).ravel()
+
+
+@pytest.mark.parametrize("variant", [None, "8", "8z", "1", "4", "8b1", "8b2u", "4b2", "gb1", "gb2u", "hb1"])
+def test_entropy_kernel_variants_count_exactly(codecs, skewed_latent, monkeypatch, variant):
+    """Every histogram kernel behind launch_hist's NIC_HIST A/B switch (256- and 1024-thread
+    blocks, 1-32 LDS replicas, zero-bin skipping, 4 or 8 loads in flight) against the oracle;
+    None = the library default."""
+    z, counts, bits_ref = skewed_latent
+    if variant is None:
+        monkeypatch.delenv("NIC_HIST", raising=False)
+    else:
+        monkeypatch.setenv("NIC_HIST", variant)
+    bits, cnt = codecs["spread"].entropy(_dev(z), counts=True)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), counts)
+    np.testing.assert_allclose(bits.cpu().numpy(), bits_ref, rtol=0, atol=2e-6)
+
+
 def test_pack_unpack_bit_exact(codecs):
     rng = np.random.default_rng(9)
     z = rng.integers(0, 256, (3, 7, 5, 96), dtype=np.uint8)
