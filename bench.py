@@ -214,9 +214,65 @@ def parity_sample(codec, x0, weights):
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` outside a launcher: start N ranks as the driver does
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) as a CHILD process
+    and return its exit code.  Runs before anything touches the GPU (no exec from a process
+    that initialised HIP)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this image
+    return subprocess.run(cmd, env=env).returncode
+
+
+def world_from_env(gpus):
+    """(world, rank, local_rank) of this process.  `--gpus` and the launcher's WORLD_SIZE must
+    agree: a mismatch is an error, never a silent 1-GPU run."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if gpus is not None and gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} ranks were launched "
+                         f"(run `python bench.py --gpus {gpus}` without a launcher, or "
+                         f"torch.distributed.run --nproc-per-node {gpus})")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def launch_check(world: int, rank: int) -> None:
+    """--launch-check: the ranks and process group of a `--gpus N` run without the codec (the
+    CPU test of the launcher; gloo).  Rank 0 prints one JSON line with n_gpus = world."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group(os.environ.get("NIC_BENCH_BACKEND", "nccl"))
+        t = torch.tensor([1.0])
+        dist.all_reduce(t)
+        ranks = int(t.item())
+        dist.destroy_process_group()
+    else:
+        ranks = 1
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_joined": ranks,
+                          "parallelism": f"dp{world}"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); without a launcher, N > 1 starts N ranks under "
+                         "torch.distributed.run; under a launcher it must equal WORLD_SIZE")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and the process group only (no GPU work) and print n_gpus")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10,
                     help="untimed steps first: kernel durations settle over the first ~15 steps (clocks)")
@@ -239,6 +295,14 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-layer HBM bytes per launch from the rocprofv3 PMC pass")
     args = ap.parse_args()
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env(args.gpus)
+    if args.launch_check:
+        launch_check(world, rank)
+        return
 
     import torch
     import torch.distributed as dist
@@ -246,15 +310,16 @@ def main():
     from neural_network_image_compression_amd import weights as W
     from neural_network_image_compression_amd.codec import Codec
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("NIC_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if world > 1 and backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {ndev} visible "
+                         "(NIC_BENCH_BACKEND=gloo shares one GPU between ranks for tests)")
     # one process per GPU; ranks beyond the visible GPUs share them round-robin (the 1-GPU
     # test box runs the world > 1 path this way, with NIC_BENCH_BACKEND=gloo)
-    dev_idx = local % max(1, torch.cuda.device_count())
+    dev_idx = local % max(1, ndev)
     torch.cuda.set_device(dev_idx)
     device = torch.device(f"cuda:{dev_idx}")
-    backend = os.environ.get("NIC_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
     coll_dev = device if backend == "nccl" else torch.device("cpu")  # gloo: host tensors
     if world > 1:
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)

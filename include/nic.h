@@ -74,6 +74,9 @@ enum {
  *     v_mfma_f32_16x16x32_f16 / v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Error
  *     ~2^-22 relative per product, i.e. at the level of fp32 accumulation-order
  *     differences.  The split format holds |x| < 65504 (the f16 range): see the range guard.
+ *     Its kernels use 32-bit offsets inside one plane: images whose 64-channel level
+ *     (ceil(h/4) x ceil(w/4), resp. 2*h8 x 2*w8 for decode) exceeds 2^22 pixels (~67 MP per
+ *     image) run the NIC_PRECISION_FP32 kernels instead (same results class, no error).
  * Bias, activations, residuals, colour transforms and quantisers are fp32 in both modes. */
 enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
 

@@ -263,8 +263,8 @@ struct nic_ctx {
   // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
   uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
-  // f16 range guard (nic.h NIC_RANGE_*): device words [flag, re-run count, and the chained
-  // re-run's grid-barrier pair], the epoch of the
+  // f16 range guard (nic.h NIC_RANGE_*): device words [flag, re-run count, the chained
+  // re-run's grid barrier (arrivals, generation, timeout flag)], the epoch of the
   // latest split-f16 pass, the policy, a pinned host word for the ERROR policy's check
   int* range = nullptr;
   int* range_host = nullptr;
@@ -498,7 +498,7 @@ int nic_create(int device, nic_ctx** out) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
   }
-  if (hipMalloc(&c->range, 4 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 4 * sizeof(int)) != hipSuccess ||
+  if (hipMalloc(&c->range, 8 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(int)) != hipSuccess ||
       hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: range-guard allocation failed");
@@ -848,9 +848,15 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
 // report to the ctx's flag word under a fresh epoch; then either the exact-fp32 re-run is
 // queued behind it, gated on that epoch (FALLBACK: stream-ordered, no host sync), or the
 // stream is synchronised and a tripped pass returns NIC_ERANGE (ERROR).
+// The split-f16 kernels address one plane's 64-channel split activation (and dconv7's
+// projections) with 32-bit buffer offsets: a plane of the 64-channel levels (h/4 x w/4,
+// resp. 2h8 x 2w8) must stay under 2^30 bytes, i.e. about 67 MP per image.  Larger images
+// run the exact-fp32 kernels (64-bit addressing) instead of failing (nic.h).
+bool x3_plane_fits(long long h64, long long w64) { return h64 * w64 * 64 * 4 < (1LL << 30); }
+
 template <class Pass>
-int guarded(nic_ctx* c, hipStream_t st, const char* what, Pass pass) {
-  if (c->precision != NIC_PRECISION_F16X3) return pass(false, RangeGuard{}, true);
+int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pass) {
+  if (c->precision != NIC_PRECISION_F16X3 || !x3_fits) return pass(false, RangeGuard{}, true);
   if (++c->epoch <= 0) c->epoch = 1;  // the flag word starts at 0: never a live epoch
   RangeGuard prod{};
   prod.flag = c->range;
@@ -1011,7 +1017,8 @@ int nic_encode(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* lat
   if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode: batch %d exceeds 21845 images per call", n);
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  return guarded(c, st, "nic_encode", [&](bool x3, const RangeGuard& rg, bool timed) {
+  const EncGeom eg = enc_geom(n, h, w);
+  return guarded(c, st, "nic_encode", x3_plane_fits(eg.c2y.out, eg.c2x.out), [&](bool x3, const RangeGuard& rg, bool timed) {
     return encode_pass(c, rgb, n, h, w, latent, prequant, st, x3, rg, timed);
   });
 }
@@ -1026,7 +1033,7 @@ int nic_decode(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_t
   if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_decode: batch %d exceeds 21845 images per call", n);
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
-  return guarded(c, st, "nic_decode", [&](bool x3, const RangeGuard& rg, bool timed) {
+  return guarded(c, st, "nic_decode", x3_plane_fits(2LL * h8, 2LL * w8), [&](bool x3, const RangeGuard& rg, bool timed) {
     return decode_pass(c, latent, n, h8, w8, rgb, rgb_f32, st, x3, rg, timed);
   });
 }
@@ -1041,10 +1048,12 @@ int nic_encode_host(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t
   if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode_host: batch %d exceeds 21845 images per call", n);
   int h8, w8;
   nic_latent_shape(h, w, &h8, &w8);
+  const EncGeom eg = enc_geom(1, h, w);
+  const bool fits = x3_plane_fits(eg.c2y.out, eg.c2x.out);
   DeviceGuard guard(c->device);
   return host_pipeline(c, rgb, (size_t)h * w * 3, latent, (size_t)h8 * w8 * 96, n, chunks, (hipStream_t)stream,
                        [&](const uint8_t* x, int m, uint8_t* z, hipStream_t st) {
-                         return guarded(c, st, "nic_encode_host", [&](bool x3, const RangeGuard& rg, bool timed) {
+                         return guarded(c, st, "nic_encode_host", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
                            return encode_pass(c, x, m, h, w, z, nullptr, st, x3, rg, timed);
                          });
                        });
@@ -1061,7 +1070,7 @@ int nic_decode_host(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, ui
   DeviceGuard guard(c->device);
   return host_pipeline(c, latent, (size_t)h8 * w8 * 96, rgb, (size_t)64 * h8 * w8 * 3, n, chunks, (hipStream_t)stream,
                        [&](const uint8_t* z, int m, uint8_t* x, hipStream_t st) {
-                         return guarded(c, st, "nic_decode_host", [&](bool x3, const RangeGuard& rg, bool timed) {
+                         return guarded(c, st, "nic_decode_host", x3_plane_fits(2LL * h8, 2LL * w8), [&](bool x3, const RangeGuard& rg, bool timed) {
                            return decode_pass(c, z, m, h8, w8, x, nullptr, st, x3, rg, timed);
                          });
                        });
@@ -1248,9 +1257,12 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   if (!c || !passes) return fail(NIC_EINVAL, "nic_range_trips: NULL argument");
   DeviceGuard guard(c->device);
   HIP_TRY(hipDeviceSynchronize());
-  int reruns = 0;
-  HIP_TRY(hipMemcpy(&reruns, c->range + 1, sizeof(int), hipMemcpyDeviceToHost));
-  *passes = (int64_t)reruns + c->error_trips;
+  int words[5] = {};
+  HIP_TRY(hipMemcpy(words, c->range, sizeof(words), hipMemcpyDeviceToHost));
+  *passes = (int64_t)words[1] + c->error_trips;
+  if (words[4])  // fp32_chain_kernel's grid barrier gave up (nic_kernels.hip grid_barrier)
+    return fail(NIC_EHIP, "nic_range_trips: a chained exact-fp32 re-run timed out at its grid barrier "
+                "(blocks not co-resident); its outputs are undefined");
   return NIC_OK;
 }
 

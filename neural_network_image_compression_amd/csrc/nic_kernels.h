@@ -103,7 +103,7 @@ struct Dconv8Args {
 constexpr int kChainMax = 6;
 struct Fp32Chain {
   RangeGuard gate;  // gate + trips of the re-run (the stages' own rg fields are unused)
-  int* bar;         // 2 zeroed device words: barrier arrivals, generation
+  int* bar;         // 3 zeroed device words: barrier arrivals, generation, timeout flag
   int nstage;
   int kind[kChainMax];      // LayerId; L_CONV1 -> c1, L_DCONV8 -> d8, other layers -> c[s]
   ConvArgs c[kChainMax];

@@ -425,6 +425,9 @@ template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
   __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+  // per-layer gated re-run (NIC_CHAIN=0): exit unless the split pass of this epoch tripped
+  // (the chained re-run checks the gate once in fp32_chain_kernel, not in the body)
+  if (range_gated_off(a.rg)) return;
   conv_mfma_body<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, IN_MODE, OUT_MODE, RESID>(a, lds, blockIdx.x, gridDim.x);
 }
 
@@ -3313,9 +3316,16 @@ constexpr int kChainLds = std::max({max_lds_floats<G_c2, G_k3, G_c8, G_d1, G_d7>
 
 // grid barrier over nb blocks: bar[0] arrivals (back to 0 after every barrier), bar[1]
 // generation.  Vector atomics and agent-scope fences (stage outputs visible across XCDs).
-__device__ __forceinline__ void grid_barrier(int* bar, int nb) {
+// The wait is bounded: the launch guarantees co-residency (cooperative launch, grid <= CUs x
+// the occupancy checked on the host), but should a block never arrive the waiters give up
+// after ~2 s (s_memrealtime, 100 MHz), set bar[2] (nic_range_trips reports it as NIC_EHIP)
+// and the kernel exits instead of hanging the queue.  Returns false after a timeout.
+constexpr unsigned long long kBarrierTimeoutTicks = 200000000ull;
+__device__ __forceinline__ bool grid_barrier(int* bar, int nb) {
+  __shared__ int ok;
   __syncthreads();
   if (threadIdx.x == 0) {
+    ok = 1;
     const int gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __threadfence();  // release this block's stage outputs
     if (atomicAdd(bar, 1) == nb - 1) {
@@ -3323,11 +3333,20 @@ __device__ __forceinline__ void grid_barrier(int* bar, int nb) {
       __threadfence();
       atomicAdd(bar + 1, 1);
     } else {
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) __builtin_amdgcn_s_sleep(2);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kBarrierTimeoutTicks) {
+          atomicExch(bar + 2, 1);  // vector atomic
+          ok = 0;
+          break;
+        }
+      }
     }
     __threadfence();  // acquire the other blocks' outputs
   }
   __syncthreads();
+  return ok != 0;
 }
 
 __global__ __launch_bounds__(256) void fp32_chain_kernel(Fp32Chain ch) {
@@ -3335,7 +3354,7 @@ __global__ __launch_bounds__(256) void fp32_chain_kernel(Fp32Chain ch) {
   if (range_gated_off(ch.gate)) return;  // whole grid: the gate word is the same for every block
   const int b0 = blockIdx.x, nb = gridDim.x;
   for (int s = 0; s < ch.nstage; ++s) {
-    if (s > 0) grid_barrier(ch.bar, nb);
+    if (s > 0 && !grid_barrier(ch.bar, nb)) return;
     const ConvArgs& a = ch.c[s];
     switch (ch.kind[s]) {
       case L_CONV1: conv1_colour_body(ch.c1, lds, b0, nb); break;
@@ -3390,14 +3409,43 @@ hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a) {
   return hipSuccess;
 }
 
+// Blocks of fp32_chain_kernel resident per CU (its LDS / VGPRs; >= 1 required), per device.
+static int chain_occupancy() {
+  static int cache[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 0;
+  if (!cache[d]) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fp32_chain_kernel, 256, 0) != hipSuccess) n = 0;
+    cache[d] = n > 0 ? n : -1;
+  }
+  return cache[d];
+}
+
+// NIC_COOP=0: plain launch of the chained re-run (A/B; co-residency then rests on the
+// occupancy check alone)
+static bool chain_cooperative() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_COOP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st) {
   if (ch.nstage == 0) return hipSuccess;
   if (!ch.bar || !ch.gate.gate) return hipErrorInvalidValue;
-  // one 256-thread block per CU (the kernel's LDS and VGPRs allow one per CU), so every
-  // block of the grid barrier can be resident; a plain launch: blocks held back by another
-  // stream's kernel start as soon as it frees its CU (nothing it waits on depends on this
-  // kernel).  (hipLaunchCooperativeKernel made the process crash at exit under rocprofv3.)
-  hipLaunchKernelGGL(fp32_chain_kernel, dim3(device_cus()), dim3(256), 0, st, ch);
+  // one 256-thread block per CU: the grid barrier needs every block resident at once, which
+  // the occupancy (>= 1 block per CU, checked) makes possible and the cooperative launch
+  // guarantees (the runtime refuses a cooperative grid that cannot be co-resident, and two
+  // contexts' cooperative kernels do not interleave their blocks on one device)
+  if (chain_occupancy() < 1) return hipErrorInvalidConfiguration;
+  const dim3 grid(device_cus()), block(256);
+  if (chain_cooperative()) {
+    void* args[] = {const_cast<Fp32Chain*>(&ch)};
+    return hipLaunchCooperativeKernel((const void*)fp32_chain_kernel, grid, block, args, 0, st);
+  }
+  hipLaunchKernelGGL(fp32_chain_kernel, grid, block, 0, st, ch);
   return hipGetLastError();
 }
 

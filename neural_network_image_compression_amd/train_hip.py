@@ -40,18 +40,29 @@ def same_pad(n: int, k: int, s: int) -> Tuple[int, int]:
     return pad // 2, pad - pad // 2
 
 
-def _stream():
-    return _torch().cuda.current_stream().cuda_stream
+def _stream(device):
+    """The current stream of the operands' device (not of the current device)."""
+    return _torch().cuda.current_stream(device).cuda_stream
+
+
+def _same_device(*ts):
+    devs = {t.device for t in ts if t is not None}
+    if len(devs) != 1:
+        raise ValueError(f"operands on different devices: {sorted(map(str, devs))}")
+    return devs.pop()
 
 
 def scale(t):
     """Device (1,) fp32 power-of-two operand scale of t (nic_absmax_scale); computed once per
-    tensor and passed to every GEMM that reads it."""
+    tensor and passed to every GEMM that reads it.  Strided views are made contiguous first
+    (the kernel reads t.numel() elements from t.data_ptr())."""
     torch = _torch()
-    out = torch.empty(1, dtype=torch.float32, device=t.device)
-    work = torch.empty(512, dtype=torch.float32, device=t.device)
-    _lib.check(_lib.lib().nic_absmax_scale(t.data_ptr(), t.numel(), out.data_ptr(), work.data_ptr(), _stream()),
-               "nic_absmax_scale")
+    t = _check(t, "scale t")
+    with torch.cuda.device(t.device):
+        out = torch.empty(1, dtype=torch.float32, device=t.device)
+        work = torch.empty(512, dtype=torch.float32, device=t.device)
+        _lib.check(_lib.lib().nic_absmax_scale(t.data_ptr(), t.numel(), out.data_ptr(), work.data_ptr(),
+                                               _stream(t.device)), "nic_absmax_scale")
     return out
 
 
@@ -71,6 +82,7 @@ def gather(x, wt, layout: int, stride: int, pad: Tuple[int, int], transposed: in
 
     x = _check(x, "gather x")
     wt = _check(wt, "gather wt")
+    dev = _same_device(x, wt, bias, sx, sw)
     n, h, w, cin = x.shape
     kh, kw = wt.shape[0], wt.shape[1]
     L = _lib.lib()
@@ -80,10 +92,12 @@ def gather(x, wt, layout: int, stride: int, pad: Tuple[int, int], transposed: in
     y = torch.empty((n, out_hw[0], out_hw[1], cout), dtype=torch.float32, device=x.device)
     sx = scale(x) if sx is None else sx
     sw = scale(wt) if sw is None else sw
-    b = _check(bias, "gather bias").data_ptr() if bias is not None else None
-    _lib.check(L.nic_conv_gather(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0], pad[1],
-                                 transposed, b, sx.data_ptr(), sw.data_ptr(), y.data_ptr(), out_hw[0], out_hw[1],
-                                 cout, work.data_ptr(), int(need.value), _stream()), "nic_conv_gather")
+    bias = _check(bias, "gather bias") if bias is not None else None
+    b = bias.data_ptr() if bias is not None else None
+    with torch.cuda.device(dev):
+        _lib.check(L.nic_conv_gather(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0], pad[1],
+                                     transposed, b, sx.data_ptr(), sw.data_ptr(), y.data_ptr(), out_hw[0], out_hw[1],
+                                     cout, work.data_ptr(), int(need.value), _stream(dev)), "nic_conv_gather")
     return y
 
 
@@ -94,6 +108,7 @@ def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int], sg=Non
 
     gat = _check(gat, "wgrad gat")
     dirt = _check(dirt, "wgrad dir")
+    dev = _same_device(gat, dirt, sg, sd)
     n, gh, gw, ca = gat.shape
     _, uh, uw, cb = dirt.shape
     L = _lib.lib()
@@ -103,9 +118,10 @@ def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int], sg=Non
     dw = torch.empty((kh, kw, ca, cb), dtype=torch.float32, device=gat.device)
     sg = scale(gat) if sg is None else sg
     sd = scale(dirt) if sd is None else sd
-    _lib.check(L.nic_conv_wgrad(gat.data_ptr(), n, gh, gw, ca, dirt.data_ptr(), uh, uw, cb, kh, kw, stride, pad[0],
-                                pad[1], sg.data_ptr(), sd.data_ptr(), dw.data_ptr(), work.data_ptr(), int(need.value),
-                                _stream()), "nic_conv_wgrad")
+    with torch.cuda.device(dev):
+        _lib.check(L.nic_conv_wgrad(gat.data_ptr(), n, gh, gw, ca, dirt.data_ptr(), uh, uw, cb, kh, kw, stride,
+                                    pad[0], pad[1], sg.data_ptr(), sd.data_ptr(), dw.data_ptr(), work.data_ptr(),
+                                    int(need.value), _stream(dev)), "nic_conv_wgrad")
     return dw
 
 
@@ -113,13 +129,16 @@ def gauss_1d(t, taps, vertical: int, adjoint: int):
     """nic_gauss_1d on one-channel planes (n, h, w)."""
     torch = _torch()
     t = _check(t, "gauss t")
+    taps = _check(taps, "gauss taps")
+    dev = _same_device(t, taps)
     n, h, w = t.shape
     d = taps.numel() - 1
     sgn = 1 if adjoint else -1
     ho, wo = (h + sgn * d, w) if vertical else (h, w + sgn * d)
     out = torch.empty((n, ho, wo), dtype=torch.float32, device=t.device)
-    _lib.check(_lib.lib().nic_gauss_1d(t.data_ptr(), n, h, w, _check(taps, "gauss taps").data_ptr(), taps.numel(),
-                                       vertical, adjoint, out.data_ptr(), ho, wo, _stream()), "nic_gauss_1d")
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().nic_gauss_1d(t.data_ptr(), n, h, w, taps.data_ptr(), taps.numel(), vertical, adjoint,
+                                           out.data_ptr(), ho, wo, _stream(dev)), "nic_gauss_1d")
     return out
 
 
@@ -131,6 +150,7 @@ def _conv_fn():
 
         @staticmethod
         def forward(ctx, x, kernel, bias, stride):
+            x, kernel = _check(x, "Conv2DSame x"), _check(kernel, "Conv2DSame kernel")
             n, h, w, _ = x.shape
             kh, kw, _, cout = kernel.shape
             pt, pl = same_pad(h, kh, stride)[0], same_pad(w, kw, stride)[0]
@@ -158,6 +178,7 @@ def _conv_fn():
 
         @staticmethod
         def forward(ctx, x, kernel, bias, stride):
+            x, kernel = _check(x, "Conv2DTransposeSame x"), _check(kernel, "Conv2DTransposeSame kernel")
             n, h, w, _ = x.shape
             kh, kw, cout, _ = kernel.shape
             oh, ow = h * stride, w * stride

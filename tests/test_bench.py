@@ -16,6 +16,47 @@ def test_bench_cli_parses():
     assert out.returncode == 0 and "--warmup" in out.stdout and "--gpus" in out.stdout
 
 
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ, NIC_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT, env=env)
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    # `python bench.py --gpus 2` with no launcher starts 2 ranks (torch.distributed.run as a
+    # child process); --launch-check stops after the process group (gloo, no GPU work)
+    out = _bench(["--gpus", "2", "--launch-check"], timeout=240)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_joined"] == 2 and d["parallelism"] == "dp2"
+
+
+def test_bench_gpus_flag_mismatch_fails():
+    # under a launcher, --gpus must equal WORLD_SIZE: never a silent 1-GPU line
+    out = _bench(["--gpus", "2", "--launch-check"], env_extra={"WORLD_SIZE": "1", "RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_without_launcher():
+    # the world-2 codec path started by `--gpus 2` alone (both ranks share the box's one GPU
+    # over gloo): rank 0's single line reports n_gpus 2 and the gathered bytes of both shards
+    out = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--no-power-probe",
+                  "--no-host-path", "--no-quality"])
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["value"] > 0
+    assert d["collectives"]["gathered_bytes"] == 8 * (32 * 32 * 96 + 256 * 256 * 3)
+
+
 @pytest.mark.gpu
 def test_bench_json_line():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",

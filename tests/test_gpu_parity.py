@@ -388,8 +388,26 @@ def test_f16_range_guard(golden, weights_spread):
     """nic.h's f16 range guard: activations past 65504 trip it; the default FALLBACK policy
     recomputes the pass with the exact-fp32 kernels on the device (results meet the golden
     contract), the ERROR policy returns NIC_ERANGE; in-range weights never trip."""
+    range_guard_contract(golden, weights_spread)
+
+
+@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "0"}], ids=["per-layer", "plain-launch"])
+def test_f16_range_guard_rerun_variants(switches):
+    """The same contract with the gated re-run as one launch per layer (NIC_CHAIN=0: every
+    fp32 kernel checks the gate itself) and as a plain (not cooperative) chained launch
+    (NIC_COOP=0); child process, the switches are read when libnic.so loads."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, **switches)
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "range_guard_check.py")
+    out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "RANGE-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+
+
+def range_guard_contract(golden, weights_spread):
     from neural_network_image_compression_amd import _lib
-    from neural_network_image_compression_amd.codec import Codec
+    from neural_network_image_compression_amd.codec import Codec, Decoder, Encoder
     g = golden("kodim21_256")
     c = Codec(0)
     assert c.precision == "f16x3"
@@ -417,6 +435,22 @@ def test_f16_range_guard(golden, weights_spread):
     assert c.range_trips() == 6
     with pytest.raises(ValueError):
         c.set_range_policy("ignore")
+    # the host-array surface (three streams, chunked): every chunk's split pass trips and its
+    # gated re-run recomputes it on the compute stream
+    c.set_range_policy("fallback")
+    enc, dec = Encoder(codec=c), Decoder(codec=c)
+    x6 = np.concatenate([g["x"]] * 6)
+    z6_ref = np.concatenate([g["latent"]] * 6)
+    enc.host_chunks = dec.host_chunks = 3
+    zh = enc(x6)
+    assert c.range_trips() == 9
+    for i in range(6):
+        check_codes(zh[i:i + 1], g["latent"], g["prequant"])
+    rh = dec(z6_ref)
+    assert c.range_trips() == 12
+    for i in range(6):
+        check_recon(rh[i:i + 1], g["recon"])
+    assert np.array_equal(zh[:1], z) and np.array_equal(rh[:1], r)
     ok = Codec(0)
     ok.set_weights(weights_spread)
     ok.set_range_policy("error")  # synchronising check, no trip

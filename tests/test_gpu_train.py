@@ -148,3 +148,22 @@ def test_ssim_gaussian_on_hip_matches_float64():
     s_ref.sum().backward()
     assert _rel_err(s_hip, s_ref) <= TOL
     assert _rel_err(xd.grad, xr.grad) <= 1e-4
+
+
+def test_strided_operands_and_scale():
+    """A strided view (not contiguous) gives the same scale and the same convolution as its
+    contiguous copy: the C-ABI reads data_ptr() / numel() of a contiguous tensor only."""
+    from neural_network_image_compression_amd import train_hip
+
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn((3, 9, 12, 64), generator=g).cuda()
+    base[:, :, :, 0] *= 1e3  # the max sits where a flat read of the view would miss it
+    view = base.permute(0, 2, 1, 3)  # (3, 12, 9, 64), strided
+    assert not view.is_contiguous()
+    assert torch.equal(train_hip.scale(view), train_hip.scale(view.contiguous()))
+    kern = (torch.randn((3, 3, 64, 64), generator=g) * 0.05).cuda()
+    y_view = train_hip.conv_same(view, kern, None, 1, act=False)
+    y_copy = train_hip.conv_same(view.contiguous(), kern, None, 1, act=False)
+    assert torch.equal(y_view, y_copy)
+    with pytest.raises(TypeError):  # a host operand never reaches the C-ABI
+        train_hip.gather(view.contiguous(), kern.cpu(), 0, 1, (1, 1), 0, (12, 9), 64)

@@ -17,7 +17,7 @@ stop_on() {  # $1 = rc, $2 = step name
 }
 
 if [[ "$STEPS" == all || "$STEPS" == *tests* ]]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x > "$OUT/${TAG}_pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 300 --timeout-method thread > "$OUT/${TAG}_pytest_gpu.log" 2>&1
   rc=$?; tail -40 "$OUT/${TAG}_pytest_gpu.log"; stop_on $rc pytest
 fi
 if [[ "$STEPS" == all || "$STEPS" == *smoke* ]]; then
