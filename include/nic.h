@@ -94,6 +94,10 @@ enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
 enum { NIC_RANGE_FALLBACK = 0, NIC_RANGE_ERROR = 1 };
 int nic_set_range_policy(nic_ctx* ctx, int policy);
 int nic_range_trips(nic_ctx* ctx, int64_t* passes);
+/* How the chained exact-fp32 re-run launches on ctx's device: its resident blocks per CU
+ * (occupancy; the grid is one block per CU and its grid barrier needs them all resident),
+ * the grid, and whether it uses a cooperative launch (1) or a plain one (0). */
+int nic_rerun_launch_info(nic_ctx* ctx, int* blocks_per_cu, int* grid, int* cooperative);
 
 /* ABI version: major * 10000 + minor * 100 + patch */
 int nic_version(void);

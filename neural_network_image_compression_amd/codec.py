@@ -121,6 +121,12 @@ class Codec:
         _lib.check(self._L.nic_range_trips(self._h, ctypes.byref(n)), "nic_range_trips")
         return int(n.value)
 
+    def rerun_launch_info(self) -> dict:
+        """How the chained exact-fp32 re-run launches here (nic_rerun_launch_info)."""
+        v = [ctypes.c_int() for _ in range(3)]
+        _lib.check(self._L.nic_rerun_launch_info(self._h, *[ctypes.byref(t) for t in v]), "nic_rerun_launch_info")
+        return {"blocks_per_cu": v[0].value, "grid": v[1].value, "cooperative": bool(v[2].value)}
+
     def set_timing(self, enable: bool) -> None:
         """Bracket every layer launch with hipEvents on the launch stream (resets the sums)."""
         _lib.check(self._L.nic_set_timing(self._h, int(bool(enable))), "nic_set_timing")

@@ -1266,6 +1266,13 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   return NIC_OK;
 }
 
+int nic_rerun_launch_info(nic_ctx* c, int* blocks_per_cu, int* grid, int* cooperative) {
+  if (!c || !blocks_per_cu || !grid || !cooperative) return fail(NIC_EINVAL, "nic_rerun_launch_info: NULL argument");
+  DeviceGuard guard(c->device);
+  fp32_chain_launch_info(blocks_per_cu, grid, cooperative);
+  return NIC_OK;
+}
+
 int nic_set_timing(nic_ctx* c, int enable) {
   if (!c) return fail(NIC_EINVAL, "nic_set_timing: NULL ctx");
   DeviceGuard guard(c->device);

@@ -8,7 +8,9 @@ namespace nic {
 // Activation formats in HBM: fp32 NHWC (exact-fp32 mode) or "split" NHWC: per pixel
 // [hi: C f16][lo: C f16] with x = hi + lo, hi = f16(x), lo = f16(x - hi) (f16x3 mode; the
 // same 4 B per element, split once by the producer's epilogue).
-enum InMode { IN_F32 = 0, IN_U8_LATENT = 1, IN_SPLIT = 2, IN_SPLIT_DMA = 3 };
+// IN_U8_CODES: the u8 latent as exact f16 codes (0..255); the 1/255 of the dequantiser is
+// folded into the epilogue scale, so the activation needs no lo half (2 MFMAs per MAC)
+enum InMode { IN_F32 = 0, IN_U8_LATENT = 1, IN_SPLIT = 2, IN_SPLIT_DMA = 3, IN_U8_CODES = 4 };
 enum OutMode { OUT_F32 = 0, OUT_U8_LATENT = 1, OUT_SPLIT = 2 };
 
 enum LayerId {
@@ -114,6 +116,7 @@ hipError_t chain_add_layer(Fp32Chain& ch, LayerId id, ConvArgs a);
 hipError_t chain_add_conv1(Fp32Chain& ch, Conv1Args a);
 hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a);
 hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st);
+void fp32_chain_launch_info(int* blocks_per_cu, int* grid, int* cooperative);  // current device
 
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA

@@ -475,7 +475,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   } while (0)
 #endif
 
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW>
+template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, bool LO = true>
 struct GeomX3 {
   static constexpr int NWAVES = WM * WN * WK;
   static constexpr int NTHREADS = 64 * NWAVES;
@@ -488,7 +488,9 @@ struct GeomX3 {
   static constexpr int NTW = NT / WN;
   static constexpr int HH = TR ? TH + 2 : (TH - 1) * S + KS;
   static constexpr int HW = TR ? TW + 2 : (TW - 1) * S + KS;
-  static constexpr int PSB = CIN * 4 + 16;  // LDS bytes per halo pixel: odd number of 16-B slots
+  // LDS bytes per halo pixel: [hi | lo | pad], or [hi | pad] for exact f16 operands (no
+  // lo half: IN_U8_CODES); an odd number of 16-B slots
+  static constexpr int PSB = CIN * (LO ? 4 : 2) + 16;
   static_assert((PSB / 16) % 2 == 1, "pixel stride must be an odd slot count");
   static constexpr int NS = CIN / 16;       // k16 steps per tap
   static constexpr int NTAPS = KS * KS;
@@ -683,6 +685,9 @@ __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int 
       const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
       if constexpr (IN_MODE == IN_F32) {
         v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * CIN + c4 * 4);
+      } else if constexpr (IN_MODE == IN_U8_CODES) {
+        const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
+        v[b][0] = __builtin_bit_cast(float, q);  // raw bytes; converted to f16 codes at the store
       } else {
         const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
         v[b][0] = u8_unit(q & 255);  // in registers: no table load per byte
@@ -698,13 +703,21 @@ __device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int 
       if (idx < TOTAL) {
         const int pix = idx / C4, c4 = idx - pix * C4;
         const int hy = pix / G::HW, hx = pix - hy * G::HW;
-        f32x4 x = v[b];
-        if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
-        f16x4 hi, lo;
-        split4(x, hi, lo);
         char* d = lds + G::pix_off(hy, hx) + c4 * 8;
-        *(f16x4*)d = hi;
-        *(f16x4*)(d + CIN * 2) = lo;
+        if constexpr (IN_MODE == IN_U8_CODES) {
+          // codes 0..255 are exact in f16: (float)byte -> f16, no split
+          const uint32_t q = inside[b] ? __builtin_bit_cast(uint32_t, v[b][0]) : 0u;
+          const f16x4 c = {(_Float16)(float)(q & 255), (_Float16)(float)((q >> 8) & 255),
+                           (_Float16)(float)((q >> 16) & 255), (_Float16)(float)(q >> 24)};
+          *(f16x4*)d = c;
+        } else {
+          f32x4 x = v[b];
+          if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
+          f16x4 hi, lo;
+          split4(x, hi, lo);
+          *(f16x4*)d = hi;
+          *(f16x4*)(d + CIN * 2) = lo;
+        }
       }
     }
   }
@@ -722,13 +735,13 @@ __device__ __forceinline__ void load_b_x3(f16x8 (&b)[NS][2][NTW], const char* wt
         b[s][hl][j] = *(const f16x8*)(wt + ((s * 2 + hl) * 2 * COUT + (wn * NTW + j) * 32) * 16);
 }
 
-template <int MTW, int CIN>
+template <int MTW, int CIN, bool LO = true>
 __device__ __forceinline__ void load_a_x3(f16x8 (&ahi)[MTW], f16x8 (&alo)[MTW], const char* lds, const int (&a_off)[MTW],
                                           int off) {
 #pragma unroll
   for (int i = 0; i < MTW; ++i) {
     ahi[i] = *(const f16x8*)(lds + a_off[i] + off);
-    alo[i] = *(const f16x8*)(lds + a_off[i] + off + CIN * 2);
+    if constexpr (LO) alo[i] = *(const f16x8*)(lds + a_off[i] + off + CIN * 2);
   }
 }
 
@@ -738,7 +751,8 @@ __device__ __forceinline__ void load_a_x3(f16x8 (&ahi)[MTW], f16x8 (&alo)[MTW], 
 // consecutive channels -- the epilogue then writes 16-B vectors.  A fragments are double
 // buffered: step s+1 (or step 0 of the next tap, at offset toff_next) is read while the
 // MFMAs of step s run.
-template <int MTW, int NTW, int NS, int CIN>
+// LO = false: the activation is exact in f16 (u8 codes), its lo half is zero -- 2 MFMAs.
+template <int MTW, int NTW, int NS, int CIN, bool LO = true>
 __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 (&b)[NS][2][NTW], const char* lds,
                                            const int (&a_off)[MTW], int toff, int toff_next, f16x8 (&ahi0)[MTW],
                                            f16x8 (&alo0)[MTW]) {
@@ -750,16 +764,17 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
     f16x8(&nhi)[MTW] = (s & 1) ? ahi0 : ahi1;
     f16x8(&nlo)[MTW] = (s & 1) ? alo0 : alo1;
     if (s + 1 < NS)
-      load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff + (s + 1) * 32);
+      load_a_x3<MTW, CIN, LO>(nhi, nlo, lds, a_off, toff + (s + 1) * 32);
     else
-      load_a_x3<MTW, CIN>(nhi, nlo, lds, a_off, toff_next);
+      load_a_x3<MTW, CIN, LO>(nhi, nlo, lds, a_off, toff_next);
     NIC_FENCE();
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][1][j], chi[i], acc[i][j], 0, 0, 0);  // w_lo*a_hi
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);  // w_hi*a_lo
+        if constexpr (LO)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);  // w_hi*a_lo
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], chi[i], acc[i][j], 0, 0, 0);  // w_hi*a_hi
       }
     NIC_FENCE();
@@ -768,7 +783,7 @@ __device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 
 #pragma unroll
     for (int i = 0; i < MTW; ++i) {
       ahi0[i] = ahi1[i];
-      alo0[i] = alo1[i];
+      if constexpr (LO) alo0[i] = alo1[i];
     }
   }
 }
@@ -865,7 +880,8 @@ __device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, c
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, int IN_MODE,
           int OUT_MODE, bool RESID>
 __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) {
-  using G = GeomX3<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW>;
+  constexpr bool LO = IN_MODE != IN_U8_CODES;  // u8 codes: exact f16 activations, 2 MFMAs per MAC
+  using G = GeomX3<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW, LO>;
   constexpr int NS = G::NS, NTW = G::NTW;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
 
@@ -920,7 +936,9 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
     a_off[i] = (TR || S == 1) ? G::pix_off(my[i], mx[i]) + half * 16
                               : my[i] * 2 * G::RPB + mx[i] * G::PSB + half * 16;
   }
-  const float scale = a.wscale[model];
+  // 2^-k undoes the weight pre-scale; with u8 codes as the activation it also carries the
+  // dequantiser's 1/255 (decoder.py:40): fma(sum, 2^-k fl(1/255), b), one rounding
+  const float scale = IN_MODE == IN_U8_CODES ? a.wscale[model] * 0.0039215688593685627f : a.wscale[model];
   if constexpr (IN_MODE == IN_SPLIT_DMA || (IN_MODE == IN_SPLIT && NIC_DMA_STAGE))
     dma_wait_all();  // this wave's DMAs landed; the barrier publishes all
   __syncthreads();
@@ -943,7 +961,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
   };
 
   f16x8 ahi[MTW], alo[MTW];
-  load_a_x3<MTW, CIN>(ahi, alo, lds, a_off, tap_off(t_begin));
+  load_a_x3<MTW, CIN, LO>(ahi, alo, lds, a_off, tap_off(t_begin));
 
   f32x16 acc[MTW][NTW];
   float rmax = 0.f;  // range guard of the split output
@@ -962,11 +980,11 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) 
       const int t2 = t + 2 < t_end ? t + 2 : t_end - 1;
       load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)t1 * TAP_BYTES, wn);
       NIC_FENCE();
-      mma_tap_x3<MTW, NTW, NS, CIN>(acc, bc, lds, a_off, tap_off(t), tap_off(t1), ahi, alo);
+      mma_tap_x3<MTW, NTW, NS, CIN, LO>(acc, bc, lds, a_off, tap_off(t), tap_off(t1), ahi, alo);
       if (t + 1 < te) {
         load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t2 * TAP_BYTES, wn);
         NIC_FENCE();
-        mma_tap_x3<MTW, NTW, NS, CIN>(acc, bn, lds, a_off, tap_off(t1), tap_off(t2), ahi, alo);
+        mma_tap_x3<MTW, NTW, NS, CIN, LO>(acc, bn, lds, a_off, tap_off(t1), tap_off(t2), ahi, alo);
       } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
@@ -3422,26 +3440,43 @@ static int chain_occupancy() {
   return cache[d];
 }
 
-// NIC_COOP=0: plain launch of the chained re-run (A/B; co-residency then rests on the
-// occupancy check alone)
-static bool chain_cooperative() {
-  static const bool on = [] {
+// NIC_COOP=1 forces the cooperative launch of the chained re-run, NIC_COOP=0 the plain one
+// (A/B); default: plain when two chains fit per CU (see launch_fp32_chain)
+static int chain_coop_switch() {
+  static const int v = [] {
     const char* e = getenv("NIC_COOP");
-    return !(e && e[0] == '0');
+    return !e ? -1 : e[0] == '0' ? 0 : 1;
   }();
-  return on;
+  return v;
+}
+
+void fp32_chain_launch_info(int* blocks_per_cu, int* grid, int* cooperative) {
+  const int occ = chain_occupancy();
+  const int sw = chain_coop_switch();
+  *blocks_per_cu = occ;
+  *grid = device_cus();
+  *cooperative = (sw == 1 || (sw < 0 && occ < 2)) ? 1 : 0;
 }
 
 hipError_t launch_fp32_chain(const Fp32Chain& ch, hipStream_t st) {
   if (ch.nstage == 0) return hipSuccess;
   if (!ch.bar || !ch.gate.gate) return hipErrorInvalidValue;
-  // one 256-thread block per CU: the grid barrier needs every block resident at once, which
-  // the occupancy (>= 1 block per CU, checked) makes possible and the cooperative launch
-  // guarantees (the runtime refuses a cooperative grid that cannot be co-resident, and two
-  // contexts' cooperative kernels do not interleave their blocks on one device)
-  if (chain_occupancy() < 1) return hipErrorInvalidConfiguration;
+  // One 256-thread block per CU; the grid barrier needs every block resident at once.
+  // occupancy >= 1 makes that possible on an idle device.  Kernels of other streams only
+  // delay blocks (they finish without waiting on the chain); what could deadlock is two
+  // chains (two contexts tripping at once) splitting the CUs.  The chain's LDS (49 KB) and
+  // VGPRs allow 3 blocks per CU, so with occupancy >= 2 two chains are co-resident and the
+  // plain launch is safe.  Below that the cooperative launch guarantees co-residency.  It
+  // is not the default: the runtime serialises a cooperative dispatch against the other
+  // streams -- the three-stream host-array surface fell from 1,977 to 1,411 MP/s -- and
+  // under rocprofv3 the process then segfaults in exit() after the profiler's finalisation
+  // (profiles/r3a_coop_rocprof_exit_crash.txt: the kernel trace is complete; the fault is
+  // in the runtime's atexit teardown).  The barrier's bounded wait catches anything else.
+  const int occ = chain_occupancy();
+  if (occ < 1) return hipErrorInvalidConfiguration;
   const dim3 grid(device_cus()), block(256);
-  if (chain_cooperative()) {
+  const int sw = chain_coop_switch();
+  if (sw == 1 || (sw < 0 && occ < 2)) {
     void* args[] = {const_cast<Fp32Chain*>(&ch)};
     return hipLaunchCooperativeKernel((const void*)fp32_chain_kernel, grid, block, args, 0, st);
   }
@@ -3688,7 +3723,7 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
 static int dconv1_variant() {
   static const int v = [] {
     const char* e = getenv("NIC_D1");
-    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : 0;
+    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5 : 0;
   }();
   return v;
 }
@@ -3716,7 +3751,10 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
         case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
         case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
         case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
-        default: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        case 5: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        // default: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
+        // epilogue); NIC_D1=s the split dequantised activations (3 MFMAs, round 2)
+        default: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
       }
     case L_DCONV5:
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);

@@ -12,6 +12,8 @@ Parity contract, stated per test:
 Parity against TensorFlow itself is unpinned (no TF, no reference fixtures): the oracle
 stands in for it, see oracle/nic_oracle.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -391,11 +393,12 @@ def test_f16_range_guard(golden, weights_spread):
     range_guard_contract(golden, weights_spread)
 
 
-@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "0"}], ids=["per-layer", "plain-launch"])
+@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "1"}], ids=["per-layer", "cooperative"])
 def test_f16_range_guard_rerun_variants(switches):
     """The same contract with the gated re-run as one launch per layer (NIC_CHAIN=0: every
-    fp32 kernel checks the gate itself) and as a plain (not cooperative) chained launch
-    (NIC_COOP=0); child process, the switches are read when libnic.so loads."""
+    fp32 kernel checks the gate itself) and as a cooperative chained launch (NIC_COOP=1; the
+    default is a plain launch, see launch_fp32_chain); child process, the switches are read
+    when libnic.so loads."""
     import os
     import subprocess
     import sys
@@ -451,6 +454,11 @@ def range_guard_contract(golden, weights_spread):
     for i in range(6):
         check_recon(rh[i:i + 1], g["recon"])
     assert np.array_equal(zh[:1], z) and np.array_equal(rh[:1], r)
+    info = c.rerun_launch_info()
+    # one block per CU; two chains (two contexts tripping at once) fit per CU, so the
+    # default plain launch cannot deadlock (launch_fp32_chain)
+    assert info["blocks_per_cu"] >= 2 and info["grid"] == torch.cuda.get_device_properties(0).multi_processor_count
+    assert info["cooperative"] == (os.environ.get("NIC_COOP") == "1")
     ok = Codec(0)
     ok.set_weights(weights_spread)
     ok.set_range_policy("error")  # synchronising check, no trip
