@@ -2638,6 +2638,9 @@ __device__ __forceinline__ void d8_store_rgb(const Dconv8Args& a, int n, int my,
 }
 
 constexpr int D8_LDS_FLOATS = D8_HH * D8_HW * D8_PS;
+// UNR: channel-quad unroll (2 in the standalone kernel; 1 inside fp32_chain_kernel, whose
+// register budget is that of two resident blocks per CU)
+template <int UNR = 2>
 __device__ __forceinline__ void dconv8_colour_body(const Dconv8Args& a, float* halo, int b0, int nb) {
   const int per_img = a.tiles_y * a.tiles_x;
   for (int job = b0; job < per_img * a.nimg; job += nb) {  // grid-stride, as conv_mfma
@@ -2668,7 +2671,7 @@ __device__ __forceinline__ void dconv8_colour_body(const Dconv8Args& a, float* h
       d8_load(pre, a, nt * a.nimg + n, ((step + 1) & 1) * D8_CC, t0y, t0x);
     }
     const float* __restrict__ w = a.w + model * 25 * 64 + c0;  // [phase-tap][ci]
-#pragma unroll 2
+#pragma unroll UNR
     for (int c4 = 0; c4 < D8_C4; ++c4) {
       f32x4 x[3][3];
 #pragma unroll
@@ -3367,7 +3370,7 @@ __device__ __forceinline__ bool grid_barrier(int* bar, int nb) {
   return ok != 0;
 }
 
-__global__ __launch_bounds__(256) void fp32_chain_kernel(Fp32Chain ch) {
+__global__ __launch_bounds__(256, 2) void fp32_chain_kernel(Fp32Chain ch) {
   __shared__ __attribute__((aligned(16))) float lds[kChainLds];
   if (range_gated_off(ch.gate)) return;  // whole grid: the gate word is the same for every block
   const int b0 = blockIdx.x, nb = gridDim.x;
@@ -3376,7 +3379,7 @@ __global__ __launch_bounds__(256) void fp32_chain_kernel(Fp32Chain ch) {
     const ConvArgs& a = ch.c[s];
     switch (ch.kind[s]) {
       case L_CONV1: conv1_colour_body(ch.c1, lds, b0, nb); break;
-      case L_DCONV8: dconv8_colour_body(ch.d8, lds, b0, nb); break;
+      case L_DCONV8: dconv8_colour_body<1>(ch.d8, lds, b0, nb); break;
       case L_CONV2: conv_mfma_body<32, 64, 5, 2, false, 8, 8, 2, 2, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
       case L_CONV3:
       case L_DCONV5: conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
