@@ -2786,6 +2786,172 @@ __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
 }
 
 // ------------------------------------------------------------------------------------
+// dconv8 gather through LDS (default; NIC_D8G=d selects dconv8_gather_kernel above).  The
+// direct gather issues 75 dword loads per thread (3 planes x 25 phase taps), each wave
+// instruction touching 8 row pieces of up to 4 projection tiles: it ran at 4.3 TB/s, bound
+// by memory instructions, not bytes.  Here a block (the same 16 x 16 coarse positions m, one
+// image) first copies, per plane, the projections its outputs read into LDS: the four phase
+// tiles of its own 8 x 8 dconv7 tile (4 x 6,400 contiguous bytes, one 16-B load per lane
+// and 400 B) and the edge row / column / corner of the neighbouring tiles that some phase
+// taps reach (489 values, a compile-time list: a window row iy = 0 reaches the row above
+// for odd phase rows, iy = 2 the row below for even ones, likewise columns), then sums each
+// output's 4..9 projections from LDS in the direct kernel's order (bit-identical results).
+// LDS image per plane: S[ph7][tap][ry][rx], 9 x 9 coarse positions per (phase, tap): rows
+// 8 ty - py7 .. 8 ty + 8 - py7 (the extra row on the side that phase reaches), same for x.
+// The next plane's loads are in flight (registers) while this plane is summed.
+// ------------------------------------------------------------------------------------
+constexpr int D8G_TB[4] = {0, 4, 10, 16};  // phase-major tap bases (dconv8's phase windows)
+constexpr int D8G_S = 4 * 25 * 81;         // floats of one plane's LDS image
+constexpr int D8G_EDGE_MAX = 512;
+struct D8gEdges {
+  unsigned e[D8G_EDGE_MAX];
+  int n;
+};
+// edge entry: bits 0..12 LDS index, 13..23 source float offset inside the tile block
+// (tap * 64 + ly * 8 + lx), 24..25 phase, 26..27 tile row delta + 1, 28..29 tile column delta + 1
+constexpr D8gEdges d8g_edges() {
+  D8gEdges E{};
+  for (int ph7 = 0; ph7 < 4; ++ph7) {
+    const int py7 = ph7 >> 1, px7 = ph7 & 1;
+    const int rye = py7 ? 0 : 8, rxe = px7 ? 0 : 8;
+    const int dty = py7 ? -1 : 1, dtx = px7 ? -1 : 1;
+    const int ly_e = py7 ? 7 : 0, lx_e = px7 ? 7 : 0;
+    for (int ph8 = 0; ph8 < 4; ++ph8) {
+      const int py8 = ph8 >> 1, px8 = ph8 & 1;
+      for (int iy = 0; iy < 2 + py8; ++iy)
+        for (int ix = 0; ix < 2 + px8; ++ix) {
+          const int t = D8G_TB[ph8] + iy * (2 + px8) + ix;
+          const bool row = iy == (py7 ? 0 : 2), col = ix == (px7 ? 0 : 2);
+          auto add = [&](int ry, int rx, int dy, int dx, int ly, int lx) {
+            E.e[E.n++] = (unsigned)(((ph7 * 25 + t) * 9 + ry) * 9 + rx) | (unsigned)(t * 64 + ly * 8 + lx) << 13 |
+                         (unsigned)ph7 << 24 | (unsigned)(dy + 1) << 26 | (unsigned)(dx + 1) << 28;
+          };
+          if (row)
+            for (int lx = 0; lx < 8; ++lx) add(rye, lx + px7, dty, 0, ly_e, lx);
+          if (col)
+            for (int ly = 0; ly < 8; ++ly) add(ly + py7, rxe, 0, dtx, ly, lx_e);
+          if (row && col) add(rye, rxe, dty, dtx, ly_e, lx_e);
+        }
+    }
+  }
+  return E;
+}
+constexpr D8gEdges kD8gEdges = d8g_edges();
+static_assert(kD8gEdges.n == 489 && kD8gEdges.n <= D8G_EDGE_MAX, "edge list");
+__constant__ unsigned c_d8g_edges[D8G_EDGE_MAX];
+constexpr int D8G_EDGES_PER_THREAD = (kD8gEdges.n + 255) / 256;
+constexpr int D8G_CENTRAL_PER_THREAD = (4 * 25 * 16 + 255) / 256;  // float4 of the 4 phase tiles
+
+constexpr int floordiv2(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+
+// sums of one plane for a thread at coarse position (2 ay + PY, 2 ax + PX) of the block
+template <int PY, int PX>
+__device__ __forceinline__ void d8g_sum(const float* S, int base, float (&acc)[4]) {
+  static_for<4>([&](auto ph8c) {
+    constexpr int ph8 = decltype(ph8c)::value, py8 = ph8 >> 1, px8 = ph8 & 1;
+    static_for<2 + py8>([&](auto iyc) {
+      constexpr int iy = decltype(iyc)::value;
+      static_for<2 + px8>([&](auto ixc) {
+        constexpr int ix = decltype(ixc)::value;
+        constexpr int t = D8G_TB[ph8] + iy * (2 + px8) + ix;
+        constexpr int py7 = (PY + 1 + iy) & 1, px7 = (PX + 1 + ix) & 1;
+        constexpr int RY = floordiv2(PY - 1 + iy) + py7, RX = floordiv2(PX - 1 + ix) + px7;
+        constexpr int C = ((py7 * 2 + px7) * 25 + t) * 81 + RY * 9 + RX;
+        acc[ph8] = __fadd_rn(acc[ph8], S[base + C]);
+      });
+    });
+  });
+}
+
+__global__ __launch_bounds__(256) void dconv8_gather_lds_kernel(Dconv8Args a) {
+  __shared__ float S[D8G_S];
+  // XCD-contiguous (image, tile) ranges, as dconv8_gather_kernel
+  const int gx = gridDim.x, total = gx * gridDim.y, L = blockIdx.y * gx + blockIdx.x;
+  const int T = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+  const int n = T / gx, tb = T - n * gx;
+  const int ty = tb / a.tiles_x7, tx = tb - ty * a.tiles_x7;
+  const int h2 = a.H >> 1, w2 = a.W >> 1;  // dconv7's coarse grid (per phase)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const unsigned plane_floats = 4u * a.tiles_y7 * a.tiles_x7 * (25u * 64u);
+  const unsigned tile_stride = 25u * 64u;
+
+  // this thread's central float4s: q = tid + 256 k -> phase q / 400, tap, row, 4 columns
+  unsigned c_off[D8G_CENTRAL_PER_THREAD];
+  int c_lds[D8G_CENTRAL_PER_THREAD], c_lim[D8G_CENTRAL_PER_THREAD];
+#pragma unroll
+  for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k) {
+    const int q = tid + 256 * k;
+    const int ph7 = q / 400, r = q - ph7 * 400, t = r >> 4, w = r & 15, ly = w >> 1, lx0 = (w & 1) * 4;
+    const bool ok = q < 1600 && 8 * ty + ly < h2;
+    c_off[k] = ok ? ((unsigned)((ph7 * a.tiles_y7 + ty) * a.tiles_x7 + tx) * tile_stride + (unsigned)(t * 64 + ly * 8 + lx0)) * 4u
+                  : kDmaOOR;
+    c_lds[k] = q < 1600 ? ((ph7 * 25 + t) * 9 + ly + (ph7 >> 1)) * 9 + lx0 + (ph7 & 1) : -1;
+    c_lim[k] = w2 - (8 * tx + lx0);  // columns j < c_lim are inside the image
+  }
+  unsigned e_off[D8G_EDGES_PER_THREAD];
+  int e_lds[D8G_EDGES_PER_THREAD];
+#pragma unroll
+  for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k) {
+    const int i = tid + 256 * k;
+    e_lds[k] = -1;
+    e_off[k] = kDmaOOR;
+    if (i < kD8gEdges.n) {
+      const unsigned e = c_d8g_edges[i];
+      const int ph7 = (e >> 24) & 3, ety = ty + (int)((e >> 26) & 3) - 1, etx = tx + (int)((e >> 28) & 3) - 1;
+      const int so = (e >> 13) & 2047, ly = (so >> 3) & 7, lx = so & 7;
+      e_lds[k] = (int)(e & 8191);
+      if ((unsigned)ety < (unsigned)a.tiles_y7 && (unsigned)etx < (unsigned)a.tiles_x7 && 8 * ety + ly < h2 &&
+          8 * etx + lx < w2)
+        e_off[k] = ((unsigned)((ph7 * a.tiles_y7 + ety) * a.tiles_x7 + etx) * tile_stride + (unsigned)so) * 4u;
+    }
+  }
+
+  f32x4 cv[D8G_CENTRAL_PER_THREAD];
+  float ev[D8G_EDGES_PER_THREAD];
+  auto load_plane = [&](int type) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.proj + (size_t)(type * a.nimg + n) * plane_floats), (short)0, (int)(plane_floats * 4u), kBufWord3);
+#pragma unroll
+    for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k)
+      cv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, c_off[k], 0, 0));
+#pragma unroll
+    for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k)
+      ev[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, e_off[k], 0, 0));
+  };
+
+  // this thread's output position: wave = parity class, lane = 8 x 8 at stride 2
+  const int PYw = wave >> 1, PXw = wave & 1, ay = lane >> 3, ax = lane & 7;
+  const int my = 16 * ty + 2 * ay + PYw, mx = 16 * tx + 2 * ax + PXw;
+  const int base = ay * 9 + ax;
+  float outv[3][4];
+  load_plane(0);
+#pragma unroll
+  for (int type = 0; type < 3; ++type) {
+    if (type > 0) __syncthreads();  // the previous plane's sums are done with S
+#pragma unroll
+    for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k)
+      if (c_lds[k] >= 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[c_lds[k] + j] = j < c_lim[k] ? cv[k][j] : 0.f;
+      }
+#pragma unroll
+    for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k)
+      if (e_lds[k] >= 0) S[e_lds[k]] = ev[k];
+    __syncthreads();
+    if (type < 2) load_plane(type + 1);  // in flight while this plane is summed
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (PYw == 0 && PXw == 0) d8g_sum<0, 0>(S, base, acc);  // wave-uniform branches
+    else if (PYw == 0) d8g_sum<0, 1>(S, base, acc);
+    else if (PXw == 0) d8g_sum<1, 0>(S, base, acc);
+    else d8g_sum<1, 1>(S, base, acc);
+    const float b = a.bias[type > 0 ? 1 : 0];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
+  }
+  if (my < a.H && mx < a.W) d8_store_rgb(a, n, my, mx, outv);
+}
+
+// ------------------------------------------------------------------------------------
 // dconv8 on the matrix pipe (split-f16, v_mfma_f32_16x16x32_f16), fused with the inverse
 // colour transform and quantiser.  Per 16 coarse positions (one row segment) and plane:
 //   D[phase][px] = sum over 9 halo neighbours d and 2 channel chunks c of A_dc x B_dc,
@@ -3813,12 +3979,34 @@ hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
   return launch_ws<64, 64, 8, 8, false, true, true>(a, st);
 }
 
+// NIC_D8G=d: the direct gather (75 dword loads per thread) instead of the LDS-staged one (A/B)
+static bool d8g_direct() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_D8G");
+    return e && e[0] == 'd';
+  }();
+  return on;
+}
+
 hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st) {
   if (!a.proj || (a.H & 1) || (a.W & 1)) return hipErrorInvalidValue;
   if (a.tiles_y7 != (a.H / 2 + 7) / 8 || a.tiles_x7 != (a.W / 2 + 7) / 8) return hipErrorInvalidValue;
   const int tiles_y = (a.H + 15) / 16;
   a.tiles_x = (a.W + 15) / 16;
-  hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  if (d8g_direct()) {
+    hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  // one block per dconv7 8x8 tile and image (= 16 x 16 coarse positions of dconv8)
+  static bool uploaded[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  if (!uploaded[dev]) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_d8g_edges), kD8gEdges.e, sizeof(kD8gEdges.e));
+    if (e != hipSuccess) return e;
+    uploaded[dev] = true;
+  }
+  hipLaunchKernelGGL(dconv8_gather_lds_kernel, dim3(a.tiles_y7 * a.tiles_x7, a.nimg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -518,9 +518,9 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
             assert (tmp_path / a / f"img{i}.png").read_bytes() == (tmp_path / b / f"img{i}.png").read_bytes()
 
 
-@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}],
-                         ids=["ws0-tile", "strip"])
-def test_alternative_kernels_parity(tmp_path, switches):
+@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "d"}],
+                         ids=["ws0-tile", "strip", "gather-direct"])
+def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the
     golden contract too; they run in a child process because the switches are read when
@@ -528,7 +528,20 @@ def test_alternative_kernels_parity(tmp_path, switches):
     import os
     import subprocess
     import sys
-    env = dict(os.environ, **switches)
+    dump = str(tmp_path / "alt.npz")
+    env = dict(os.environ, NIC_ALT_DUMP=dump, **switches)
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+    if switches == {"NIC_D8G": "d"}:
+        # the LDS-staged gather sums the same projections in the same order as the direct one
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from alt_kernels_check import alt_cases
+
+        from neural_network_image_compression_amd.codec import Codec
+        c = Codec(0, precision="f16x3")
+        c.set_weights(weights_spread)
+        mine = alt_cases(c)
+        with np.load(dump) as other:
+            for k, v in mine.items():
+                np.testing.assert_array_equal(v.cpu().numpy(), other[k], err_msg=k)
