@@ -2786,7 +2786,7 @@ __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
 }
 
 // ------------------------------------------------------------------------------------
-// dconv8 gather through LDS (default; NIC_D8G=d selects dconv8_gather_kernel above).  The
+// dconv8 gather through LDS (NIC_D8G=l; the default is dconv8_gather_kernel above).  The
 // direct gather issues 75 dword loads per thread (3 planes x 25 phase taps), each wave
 // instruction touching 8 row pieces of up to 4 projection tiles: it ran at 4.3 TB/s, bound
 // by memory instructions, not bytes.  Here a block (the same 16 x 16 coarse positions m, one
@@ -2798,7 +2798,10 @@ __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
 // output's 4..9 projections from LDS in the direct kernel's order (bit-identical results).
 // LDS image per plane: S[ph7][tap][ry][rx], 9 x 9 coarse positions per (phase, tap): rows
 // 8 ty - py7 .. 8 ty + 8 - py7 (the extra row on the side that phase reaches), same for x.
-// The next plane's loads are in flight (registers) while this plane is summed.
+// The next plane's loads are in flight (registers) while this plane is summed.  Measured
+// same-box no faster than the direct gather (0.074-0.076 vs 0.072-0.075 ms, 4.3-4.5 TB/s
+// both): fewer memory instructions did not move the rate, so the direct kernel is not bound
+// by its instruction count; kept as the tested alternative.
 // ------------------------------------------------------------------------------------
 constexpr int D8G_TB[4] = {0, 4, 10, 16};  // phase-major tap bases (dconv8's phase windows)
 constexpr int D8G_S = 4 * 25 * 81;         // floats of one plane's LDS image
@@ -3979,11 +3982,12 @@ hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
   return launch_ws<64, 64, 8, 8, false, true, true>(a, st);
 }
 
-// NIC_D8G=d: the direct gather (75 dword loads per thread) instead of the LDS-staged one (A/B)
+// NIC_D8G=l: the LDS-staged gather instead of the direct one (A/B: 0.074-0.076 vs
+// 0.072-0.075 ms same-box over 3 rounds, bit-identical results -- not the default)
 static bool d8g_direct() {
   static const bool on = [] {
     const char* e = getenv("NIC_D8G");
-    return e && e[0] == 'd';
+    return !(e && e[0] == 'l');
   }();
   return on;
 }
