@@ -176,6 +176,13 @@ int nic_ms_ssim(nic_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int h, 
  * bytes_per_image bytes: sse (n,) uint64.  PSNR = 10 log10(255^2 * bytes / sse). */
 int nic_sq_err(const uint8_t* a, const uint8_t* b, int n, int64_t bytes_per_image, uint64_t* sse, void* stream);
 
+/* PNG byte count of each of m u8 images (h, w, channels = 1 or 3) in HOST memory, exactly as
+ * Pillow writes it with optimize=True (the reference's save_img, utils.py:85-87): adaptive
+ * per-row filter (least sum of |signed bytes|), zlib level 9 / window 15 / memLevel 9 /
+ * Z_FILTERED, 65,536-B IDATs.  get_bpp (training.py:12-21) is 8 * sizes[i] / pixels.  Host
+ * threads only (threads >= 1), no GPU, no ctx.  w * channels <= 16384. */
+int nic_png_sizes(const uint8_t* images, int m, int h, int w, int channels, int64_t* sizes, int threads);
+
 /* Bitstream image layout of ProClass._feed_batch: (n,h8,w8,96) <-> (n,4*h8,8*w8,3), each
  * plane a raw C-order reshape (utils.py:35-36, 39-40). */
 int nic_pack_latent(const uint8_t* latent, int n, int h8, int w8, uint8_t* packed, void* stream);

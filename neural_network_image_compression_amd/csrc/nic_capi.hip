@@ -39,6 +39,13 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+}  // namespace
+
+// the thread's error message for the C-ABI entry points outside this file (nic_png.cpp)
+int nic::set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+namespace {
+
 #define HIP_TRY(expr)                                                                         \
   do {                                                                                        \
     hipError_t _e = (expr);                                                                   \

@@ -5,6 +5,8 @@
 
 namespace nic {
 
+int set_error(int code, const char* msg);  // nic_last_error() text of this thread (nic_capi.hip)
+
 // Activation formats in HBM: fp32 NHWC (exact-fp32 mode) or "split" NHWC: per pixel
 // [hi: C f16][lo: C f16] with x = hi + lo, hi = f16(x), lo = f16(x - hi) (f16x3 mode; the
 // same 4 B per element, split once by the producer's epilogue).

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 
 import numpy as np
 
-from .bitstream import png_bytes
+from .bitstream import png_sizes
 from .codec import Codec
 from .quality import ms_ssim_supported
 
@@ -71,11 +71,8 @@ def rd_point(codec: Codec, images: np.ndarray, tile: Optional[int] = None, png: 
                               "psnr_db": codec.psnr(x_d, rec_d, per_image=True)}
     if ms_ssim_supported(h, w):
         out["ms_ssim"] = codec.ms_ssim(x_d, rec_d).cpu().numpy().astype(np.float64)
-    if png:
-        from concurrent.futures import ThreadPoolExecutor
-
-        with ThreadPoolExecutor(max_workers=max(1, workers)) as pool:
-            sizes = np.array(list(pool.map(lambda a: len(png_bytes(a)), list(packed))), dtype=np.float64)
+    if png:  # Pillow's byte counts, computed natively on host threads (bitstream.png_sizes)
+        sizes = png_sizes(packed, threads=max(1, workers)).astype(np.float64)
         if tile:
             sizes = sizes.reshape(n, -1).sum(axis=1)
         out["bpp_png"] = 8.0 * sizes / (h * w)

@@ -34,7 +34,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from . import weights as W
-from .bitstream import png_bytes
+from .bitstream import png_sizes
 
 YCBCR = ((0.299, 0.587, 0.114), (-0.16874, -0.33126, 0.5), (0.5, -0.41869, -0.08131))  # utils.py:7
 YCBCR_OFF = (0.0, 0.5, 0.5)  # utils.py:9
@@ -150,12 +150,15 @@ def ssim(x, y, max_val: float = 1.0, hip: bool = False):
     return (lum * cs).mean(dim=(1, 2, 3))
 
 
-def png_bpp_planes(encoded_u8: np.ndarray, tot_pixels: float, pool: Optional[ThreadPoolExecutor] = None) -> np.ndarray:
-    """get_bpp (training.py:14-21): latent planes (M,h,w,32) u8 -> (M,) 8*len(PNG((4h,8w)))/pixels."""
+def png_bpp_planes(encoded_u8: np.ndarray, tot_pixels: float, threads: int = 16) -> np.ndarray:
+    """get_bpp (training.py:14-21): latent planes (M,h,w,32) u8 -> (M,) 8*len(PNG((4h,8w)))/pixels.
+
+    The PNG sizes are Pillow's own byte counts (save_img's encoder, utils.py:85-87), computed
+    natively on ``threads`` host threads (bitstream.png_sizes / nic_png_sizes, tested equal to
+    Pillow byte for byte)."""
     m, h, w, _ = encoded_u8.shape
-    imgs = list(encoded_u8.reshape(m, 4 * h, 8 * w))
-    sizes = list(pool.map(png_bytes, imgs)) if pool else [png_bytes(a) for a in imgs]
-    return np.array([8.0 * len(s) / tot_pixels for s in sizes], np.float32)
+    sizes = png_sizes(encoded_u8.reshape(m, 4 * h, 8 * w), threads)
+    return (8.0 * sizes.astype(np.float64) / tot_pixels).astype(np.float32)
 
 
 class Entropynet:
@@ -221,7 +224,7 @@ class Training:
 
     def __init__(self, device: str = "cuda", weights: Optional[W.Weights] = None, seed: int = 0,
                  checkpoint_dir: str = "../checkpoints/", backend: Optional[str] = None,
-                 png_workers: Optional[int] = None):
+                 png_threads: int = 16):
         """backend "hip" (default on a GPU): every convolution of the step, forward and
         backward, on the HIP split-f16x3 MFMA kernels (train_hip, NHWC); "torch" (default on
         the CPU): PyTorch autograd convolutions (MIOpen / oneDNN, NCHW) -- the restatement the
@@ -241,9 +244,11 @@ class Training:
         self.entropy_model: Optional[Entropynet] = None
         self._opt = None
         self._gen = torch.Generator(device=self.device).manual_seed(seed)
-        # host threads for the PNG-size target (get_bpp, training.py:14-21: 3B PNG encodes per
-        # step, the step's longest stage); zlib releases the GIL
-        self._pool = ThreadPoolExecutor(max_workers=png_workers or 8)  # 16 measured slower (27.9 vs 32.7 ms per step)
+        # the PNG-size target (get_bpp, training.py:14-21: 3B PNG encodes per step) runs on
+        # host threads (nic_png_sizes) while the device runs the codec's backward: train_step
+        # needs it only for the entropy net's own loss, after the codec gradients are queued
+        self.png_threads = png_threads
+        self._pool = ThreadPoolExecutor(max_workers=1)
 
     def _model(self, name: str) -> Dict[str, object]:
         pre = name + "/"
@@ -265,13 +270,15 @@ class Training:
     def train_step(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
         """One batch (training.py:67-147): u8 NHWC images (B,H,W,3) -> metrics."""
         torch = _torch()
-        f = self.losses(images, entropy_loss_coef, flip)
-        loss0, loss1, aprox_entropy_loss = f["loss0"], f["loss1"], f["entropy_loss"]
+        f = self.losses(images, entropy_loss_coef, flip, defer_png=True)
+        loss0, loss1 = f["loss0"], f["loss1"]
         opt_y, opt_c, opt_e = self._opt
         ent_params = self.entropy_model.parameters()
-        # three tapes: main losses update the codec models only, the entropy loss the net only
+        # three tapes: main losses update the codec models only, the entropy loss the net only;
+        # the codec gradients are queued while the host threads size the PNG target
         gy = torch.autograd.grad(loss0, self._variables("Y"), retain_graph=True)
         gc = torch.autograd.grad(loss1, self._variables("CbCr"), retain_graph=True)
+        aprox_entropy_loss = self.finish_entropy_loss(f)
         ge = torch.autograd.grad(aprox_entropy_loss, ent_params)
         for opt, params, grads in ((opt_y, self._variables("Y"), gy), (opt_c, self._variables("CbCr"), gc),
                                    (opt_e, ent_params, ge)):
@@ -289,9 +296,43 @@ class Training:
                 "bpp": [float(v.mean()) for v in np.split(bpp, 3)],
                 "entropy_loss": float(aprox_entropy_loss.detach()), "loss": [float(loss0.detach()), float(loss1.detach())]}
 
-    def losses(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
+    def _png_target(self, codes, pixels: float):
+        """Start get_bpp of the step's u8 codes (M,h,w,32) on a host thread: an async copy to
+        page-locked memory, then nic_png_sizes once it has landed.  Returns a future."""
+        torch = _torch()
+        threads = self.png_threads
+        if codes.is_cuda:
+            host = torch.empty(codes.shape, dtype=torch.uint8, pin_memory=True)
+            host.copy_(codes, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+
+            def job():
+                ev.synchronize()
+                return png_bpp_planes(host.numpy(), pixels, threads)
+        else:
+            arr = codes.numpy().copy()
+
+            def job():
+                return png_bpp_planes(arr, pixels, threads)
+        return self._pool.submit(job)
+
+    def finish_entropy_loss(self, f: Dict[str, object]):
+        """The entropy net's loss (training.py:93-101) once the PNG target is in: MSE between
+        its estimate and get_bpp of the codes.  Sets f["bpp"] and f["entropy_loss"]."""
+        torch = _torch()
+        if "entropy_loss" not in f:
+            bpp = f.pop("bpp_future").result()
+            bpp_t = torch.from_numpy(bpp).to(self.device).view(-1, 1)
+            f["bpp"] = bpp
+            f["entropy_loss"] = ((bpp_t - f["aprox"]) ** 2).mean()
+        return f["entropy_loss"]
+
+    def losses(self, images, entropy_loss_coef: float, flip: bool = True, defer_png: bool = False) -> Dict[str, object]:
         """The step's forward pass (training.py:67-126): the two codec losses, the entropy
-        net's loss and the tensors the metrics read (differentiable w.r.t. the parameters)."""
+        net's loss and the tensors the metrics read (differentiable w.r.t. the parameters).
+        defer_png: leave the PNG target running (f["bpp_future"]); finish_entropy_loss
+        completes f["entropy_loss"] / f["bpp"] later."""
         torch = _torch()
         x = images.to(self.device)
         b = x.shape[0]
@@ -321,9 +362,7 @@ class Training:
         aprox = self.entropy_model(batch_enc, hip)  # (3B, 1)
         codes = torch.round(batch_enc.detach() * 255).clamp(0, 255).to(torch.uint8)
         codes = codes if hip else codes.permute(0, 2, 3, 1)
-        bpp = png_bpp_planes(codes.contiguous().cpu().numpy(), float(x.shape[1] * x.shape[2]), self._pool)
-        bpp_t = torch.from_numpy(bpp).to(self.device).view(-1, 1)
-        aprox_entropy_loss = ((bpp_t - aprox) ** 2).mean()
+        bpp_future = self._png_target(codes.contiguous(), float(x.shape[1] * x.shape[2]))
         ent = torch.split(aprox, b, dim=0)
         dec0 = base_decoder(self._model("decoderY"), noisy0, hip)
         dec1 = base_decoder(self._model("decoderCbCr"), noisy1, hip)
@@ -334,8 +373,11 @@ class Training:
         ssim1 = ssim1_each.mean()
         loss0 = ((1 - ssim0) / 2 + entropy_loss_coef * ent[0]).sum()
         loss1 = ((1 - ssim1) / 2 + 0.01 * torch.cat(ent[1:], dim=0)).sum()  # reference: 0.01 (training.py:124)
-        return {"loss0": loss0, "loss1": loss1, "entropy_loss": aprox_entropy_loss, "ssim0": ssim0,
-                "ssim1_each": ssim1_each, "bpp": bpp, "aprox": aprox}
+        f = {"loss0": loss0, "loss1": loss1, "ssim0": ssim0, "ssim1_each": ssim1_each, "aprox": aprox,
+             "bpp_future": bpp_future}
+        if not defer_png:
+            self.finish_entropy_loss(f)
+        return f
 
     def weights(self) -> W.Weights:
         return {k: v.detach().float().cpu().numpy().copy() for k, v in self.params.items()}

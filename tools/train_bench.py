@@ -3,8 +3,9 @@
 
 One step = Training.losses() forward + the three autograd.grad calls of train_step
 (tf2_0/src/training.py:74-151) on a batch of B synthetic 128x128 patches, Adam excluded.
-The PNG-size bpp target (host Pillow, training.py:12-21) is replaced by zeros here so the
-device work is what is timed (it is the same host work for both backends).
+The PNG-size bpp target (host threads, nic_png_sizes, training.py:12-21) is replaced by zeros
+unless --png, so the device work is what is timed (it is the same host work for both backends);
+with --png it overlaps the codec's backward as in Training.train_step.
 
     python tools/train_bench.py [--batch 64] [--size 128] [--steps 10] [--out gpurun_out/train_bench.json]
 """
@@ -38,7 +39,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--backends", default="hip,torch")
     ap.add_argument("--png", action="store_true", help="keep the host PNG-size target (the full step)")
-    ap.add_argument("--png-workers", type=int, default=None)
+    ap.add_argument("--png-threads", type=int, default=16)
     args = ap.parse_args()
     import torch
 
@@ -46,7 +47,7 @@ def main():
     from neural_network_image_compression_amd import weights as W
 
     if not args.png:
-        T.png_bpp_planes = lambda enc, tot, pool=None: np.zeros(enc.shape[0], np.float32)  # device work only
+        T.png_bpp_planes = lambda enc, tot, threads=None: np.zeros(enc.shape[0], np.float32)  # device work only
     g = torch.Generator().manual_seed(0)
     imgs = torch.randint(0, 256, (args.batch, args.size, args.size, 3), generator=g, dtype=torch.uint8).cuda()
     w0 = W.seeded_weights(0, init="glorot")
@@ -56,13 +57,13 @@ def main():
                    + (", host PNG target)" if args.png else ", PNG target zeroed)")}
     for be in args.backends.split(","):
         tr = T.Training(device="cuda", weights=w0, seed=0, checkpoint_dir="/tmp/nic_tb/", backend=be,
-                        png_workers=args.png_workers)
+                        png_threads=args.png_threads)
 
         def step():
-            f = tr.losses(imgs, 0.01, flip=True)
+            f = tr.losses(imgs, 0.01, flip=True, defer_png=True)
             torch.autograd.grad(f["loss0"], tr._variables("Y"), retain_graph=True)
             torch.autograd.grad(f["loss1"], tr._variables("CbCr"), retain_graph=True)
-            torch.autograd.grad(f["entropy_loss"], tr.entropy_model.parameters())
+            torch.autograd.grad(tr.finish_entropy_loss(f), tr.entropy_model.parameters())
 
         for _ in range(args.warmup):
             step()

@@ -4,12 +4,13 @@ entropy_loss_coef (SURVEY config 4: 0.01 / 0.02 / 0.03; the reference's main use
 tf2_0/src/training.py:179), then evaluate each trained set with the device RD harness
 (rd.py) on the reference's Kodak image kodim21 (768x512), whole-image and as 256^2 tiles.
 
-Data: the reference's own training patches, a 1,000-patch subset committed under
-data/imagenet_patches_1k (tools/make_train_subset.py); an epoch is --epoch-samples images
-(default 19,000 = the reference's epoch over all of data/imagenet_patches) drawn from
-reshuffled passes of the subset, so the coefficient schedule keeps the reference's pace.
+Data: the reference's own training patches.  data/imagenet_patches_full (all 19,000, copied
+by tools/make_train_subset.py --full; git- and gpurun-ignored except for the training call)
+is used when present, one epoch = one pass, as training.py:175-179; otherwise the committed
+1,000-patch subset data/imagenet_patches_1k with --epoch-samples images (default 19,000)
+per epoch drawn from reshuffled passes, so the coefficient schedule keeps the reference's pace.
 
-    python tools/train_rd.py [--epochs 10] [--batch 64] [--steps N] [--out FILE]
+    python tools/train_rd.py [--epochs 30] [--batch 64] [--steps N] [--out FILE] [--save-dir DIR]
 """
 import argparse
 import json
@@ -36,15 +37,21 @@ def load_patches(d):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--data", default=os.path.join(ROOT, "data", "imagenet_patches_1k"))
-    ap.add_argument("--epochs", type=int, default=10)
-    ap.add_argument("--epoch-samples", type=int, default=19000)
+    full = os.path.join(ROOT, "data", "imagenet_patches_full")
+    ap.add_argument("--data", default=full if os.path.isdir(full) else os.path.join(ROOT, "data", "imagenet_patches_1k"))
+    ap.add_argument("--epochs", type=int, default=30)  # training.py:179
+    ap.add_argument("--epoch-samples", type=int, default=None,
+                    help="images per epoch (default: one pass of the full set, 19,000 for the subset)")
+    ap.add_argument("--save-dir", default=None, help="write each trained set as <dir>/coefX.XX_{encoder,decoder}{Y,CbCr}.safetensors")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=0, help="stop each run after this many steps (0: all epochs)")
     ap.add_argument("--coefs", default="0.01,0.02,0.03")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     x = load_patches(args.data)
+    if args.epoch_samples is None:
+        args.epoch_samples = len(x) if len(x) >= 19000 else 19000
+    print(f"data: {len(x)} patches from {args.data}, {args.epoch_samples} images per epoch", flush=True)
     with np.load(os.path.join(ROOT, "tests", "golden", "kodim21_full.npz"), allow_pickle=False) as g:
         ev = g["x"]  # the reference's data/kodak_img/kodim21.png, (1, 512, 768, 3)
     sets, train_log = {}, {}
@@ -66,6 +73,10 @@ def main():
             w.update(W.load(os.path.join(d, "decoder"), "decoder"))
         label = f"coef{coef:.2f}"
         sets[label] = w
+        if args.save_dir:
+            os.makedirs(args.save_dir, exist_ok=True)
+            for kind in ("encoder", "decoder"):  # <dir>/<label>_encoderY.safetensors, ...
+                W.save(w, os.path.join(args.save_dir, f"{label}_{kind}"), kind)
         tail = log[-20:]
         train_log[label] = {"steps": len(log), "epochs": epochs, "seconds": round(time.perf_counter() - t0, 1),
                             "train_seconds": round(t_train, 1),
@@ -76,7 +87,7 @@ def main():
     res = rd_sweep(sets, ev, tile=256)
     out = {"config": f"config4: trained from entropy_loss_coef {args.coefs} (+0.01 per epoch, training.py:165), "
                      f"{args.epochs} epochs of {args.epoch_samples} images, batch {args.batch}, on the reference's "
-                     "ImageNet patches (1,000-patch subset); evaluated on kodim21 768x512, whole and 256^2 tiles",
+                     f"ImageNet patches ({len(x)} of them); evaluated on kodim21 768x512, whole and 256^2 tiles",
            "train": train_log, "points": {}}
     for label, modes in res.items():
         out["points"][label] = {mode: {k: (round(v, 6) if isinstance(v, float) else v) for k, v in d.items()
