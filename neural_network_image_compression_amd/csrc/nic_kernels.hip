@@ -3919,10 +3919,10 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
     case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N (NIC_D1 A/B:
                     // "16" 8x16 tile, 2 waves x 4 M tiles; "w4" 8x16 tile, 4 waves)
       switch (dconv1_variant()) {
-        case 1: return launch_x3<32, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
-        case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
-        case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
-        case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        case 1: return launch_x3<32, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_CODES, OUT_SPLIT, false>(a, st);
         case 5: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
         // default: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
         // epilogue); NIC_D1=s the split dequantised activations (3 MFMAs, round 2)

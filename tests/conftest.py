@@ -41,3 +41,16 @@ def weights_spread():
 def weights_glorot():
     from neural_network_image_compression_amd import weights as W
     return W.seeded_weights(0, init="glorot")
+
+
+@pytest.fixture(scope="session")
+def weights_trained():
+    """The coefficient-0.01 codec trained for 30 epochs on the reference's 19,000 patches
+    (tools/train_rd.py, round 3), committed under tests/golden/trained."""
+    import os
+
+    from neural_network_image_compression_amd import weights as W
+    pre = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trained", "coef0.01_")
+    w = W.load(pre + "encoder", "encoder")
+    w.update(W.load(pre + "decoder", "decoder"))
+    return w

@@ -69,10 +69,12 @@ def test_full_encoder_decoder_match_torch(golden, weights_spread):
         assert np.abs(po - pt.permute(0, 2, 3, 1).numpy()).max() <= 2e-6
 
 
-@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot"])
-def test_oracle_reproduces_golden(case, golden, manifest, weights_spread, weights_glorot):
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot", "kodim21_256_trained",
+                                  "imagenet4_trained"])
+def test_oracle_reproduces_golden(case, golden, manifest, weights_spread, weights_glorot, weights_trained):
     g = golden(case)
-    w = weights_spread if manifest["cases"][case]["init"] == "spread" else weights_glorot
+    w = {"spread": weights_spread, "glorot": weights_glorot,
+         "trained_coef0.01": weights_trained}[manifest["cases"][case]["init"]]
     f = O.encode_f32(w, g["x"])
     assert np.abs(f - g["prequant"]).max() <= 1e-6
     z = O.quantise_u8(f)
@@ -84,10 +86,11 @@ def test_oracle_reproduces_golden(case, golden, manifest, weights_spread, weight
     np.testing.assert_allclose(O.hist_entropy(g["latent"]), g["bits"], rtol=0, atol=1e-6)
 
 
-def test_weights_digest_pinned(manifest, weights_spread, weights_glorot):
+def test_weights_digest_pinned(manifest, weights_spread, weights_glorot, weights_trained):
     from neural_network_image_compression_amd import weights as W
     assert W.digest(weights_spread) == manifest["weights"]["spread"]
     assert W.digest(weights_glorot) == manifest["weights"]["glorot"]
+    assert W.digest(weights_trained) == manifest["weights"]["trained_coef0.01"]
 
 
 def test_colour_constants():
