@@ -469,6 +469,11 @@ def main():
     d78_fused = (args.precision == "f16x3" and os.environ.get("NIC_WS", "1")[:1] != "0"
                  and os.environ.get("NIC_D8", "p")[:1] not in ("t", "s"))
     moved = {"conv2": "conv1" if conv1_fused else None, "dconv7": "dconv8" if d78_fused else None}
+    # the fused k3 residual pairs (planes up to 64 columns): one launch each, timed as conv4 / dconv6
+    k3_fused = {"conv4": "conv3", "dconv6": "dconv5"}
+    for b, a_ in k3_fused.items():
+        if lt[a_][1] == 0 and lt[b][1] > 0:
+            moved[b] = a_
     flops = {}
     for name, (ms, n) in lt.items():
         if n == 0:
@@ -491,6 +496,8 @@ def main():
             layers[name]["fused"] = "conv1 (colour transform + conv1 computed into conv2's LDS halo)"
         if name == "dconv7" and d78_fused:
             layers[name]["fused"] = "dconv8's MACs (25 tap projections per output pixel, split-f16 MFMA)"
+        if moved.get(name) in ("conv3", "dconv5"):
+            layers[name]["fused"] = f"{moved[name]} -> {name} -> + residual (one launch, row-streamed through LDS)"
     if ent_ms is not None:
         nbytes = B * h8 * w8 * 96 + 3 * B * 4  # u8 latent read once + 3 floats per image
         layers["entropy"] = {"avg_ms": round(ent_ms, 4), "gbytes_per_launch": round(nbytes / 1e9, 4),

@@ -645,6 +645,16 @@ int nic_reserve(nic_ctx* c, int n, int h, int w) {
 
 namespace {
 
+// NIC_K3P=0: the k3 residual pairs as two weight-stationary launches instead of the fused one
+// (A/B; the fused kernel takes planes up to 64 columns, wider ones always use two launches)
+bool use_k3pair() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_K3P");
+    return !(e && e[0] == '0') && conv12_fused();  // conv12_fused(): the weight-stationary set (NIC_WS)
+  }();
+  return on;
+}
+
 // NIC_CHAIN=0: the gated re-run as one launch per layer (A/B)
 bool use_chain() {
   static const bool on = [] {
@@ -745,8 +755,19 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   } else {
     TIMED(L_CONV2, run(L_CONV2, a2));
   }
-  TIMED(L_CONV3, run(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1)));
-  TIMED(L_CONV4, run(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1)));
+  if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {
+    // conv3 -> conv4 -> + res as one launch (R1 -> R3, the residual read from the input
+    // rows in LDS); timed as conv4
+    ConvArgs ap = conv(L_CONV3, R[1], R[3], nullptr, h2, w2, h2, w2, 1, 1);
+    ap.wx2 = c->wx[L_CONV4];
+    ap.wscale2[0] = c->wscale[L_CONV4][0];
+    ap.wscale2[1] = c->wscale[L_CONV4][1];
+    ap.bias2 = c->wb[L_CONV4];
+    TIMED(L_CONV4, launch_k3pair_x3(ap, st));
+  } else {
+    TIMED(L_CONV3, run(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1)));
+    TIMED(L_CONV4, run(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1)));
+  }
   ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);
   a8.out_u8 = latent;
   a8.out_f32_latent = prequant;
@@ -810,8 +831,17 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   d1.rg = rg;
   TIMED(L_DCONV1, run(L_DCONV1, d1));
   const int h2 = 2 * h8, w2 = 2 * w8;
-  TIMED(L_DCONV5, run(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2)));
-  TIMED(L_DCONV6, run(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2)));
+  if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {  // dconv5 -> dconv6 -> + res, timed as dconv6
+    ConvArgs ap = conv(L_DCONV5, R[1], R[3], nullptr, h2, w2, h2, w2);
+    ap.wx2 = c->wx[L_DCONV6];
+    ap.wscale2[0] = c->wscale[L_DCONV6][0];
+    ap.wscale2[1] = c->wscale[L_DCONV6][1];
+    ap.bias2 = c->wb[L_DCONV6];
+    TIMED(L_DCONV6, launch_k3pair_x3(ap, st));
+  } else {
+    TIMED(L_DCONV5, run(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2)));
+    TIMED(L_DCONV6, run(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2)));
+  }
   ConvArgs d7 = conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2);
   // f16x3: dconv7 writes dconv8's per-pixel tap projections (100 B / pixel instead of 256)
   const bool fuse78 = x3 && dconv78_fused();

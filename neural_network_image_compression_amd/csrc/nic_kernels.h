@@ -58,6 +58,12 @@ struct ConvArgs {
   int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
   int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
+  // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
+  // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
+  const uint16_t* wx2;
+  float wscale2[2];
+  const float* bias2;
+  int seg_rows;
   // conv1 fused into conv2 (f16x3): the colour plane is computed from the RGB input and
   // conv1's split output is written straight into conv2's LDS halo (no HBM round trip)
   const uint8_t* rgb;     // [N][H0][W0][3]
@@ -123,6 +129,10 @@ void fp32_chain_launch_info(int* blocks_per_cu, int* grid, int* cooperative);  /
 hipError_t upload_constants(const float* u8_to_unit, const float* ycbcr, const float* ycbcr_inv, const float* off);
 hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st);      // exact fp32 MFMA
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // split-f16 (3-pass) MFMA
+// the residual pair x -> leaky(conv_b(leaky(conv_a(x)))) + x of two k3 s1 64-channel layers as
+// one launch (split-f16), for planes up to K3P_MAX_W columns; false: use two launches
+bool k3pair_supported(int H, int W);
+hipError_t launch_k3pair_x3(const ConvArgs& a, hipStream_t st);
 hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st);  // conv1 fused into conv2 (f16x3)
 // the fused conv1's padded colour planes: origin offsets and plane size in f16 elements
 // (a.cplane must hold 2 * P * hp * wp of them)

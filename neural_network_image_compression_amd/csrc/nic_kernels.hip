@@ -2449,6 +2449,216 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 }
 
 // ------------------------------------------------------------------------------------
+// Fused residual pair of the k3 s1 layers: out = leaky(conv_b(leaky(conv_a(x) + b_a)) + b_b) + x
+// (encoder.py:22-25 conv3 -> conv4 -> + res; decoder.py:26-29 dconv5 -> dconv6 -> + res, the
+// Conv2DTranspose k3 s1 layers repacked as flipped convs).  Split-f16 in and out.
+//
+// The two separate weight-stationary launches move, per pixel, the input with its tile halo
+// (256 B x 1.56), conv_a's output out and back in with its halo, the residual, and the
+// output: ~1.6 KB per pixel for 147 kFLOP -- at the f16x3 ridge point (833 TFLOP/s / 8 TB/s).
+// Here a block owns whole rows of one plane (planes up to K3P_MAX_W = 64 columns: the 256^2
+// images of BASELINE config 2) and streams down a segment of K3P_SR output rows:
+//   * the input rows arrive by LDS-DMA into a 5-row ring (row y+2 lands while row y+1 is
+//     being convolved), read once from HBM (+2 rows per segment);
+//   * waves 0-3 (conv_a, 16 output channels each, weights resident in VGPRs) convolve input
+//     rows y-1..y+1 into row y of a 4-row ring of conv_a outputs in LDS (split records);
+//   * waves 4-7 (conv_b) convolve rows y-3..y-1 of that ring into output row y-2, add the
+//     residual from the input ring (still resident) and store the split row to HBM.
+// One block barrier per row step.  conv_a's row never leaves the chip, the residual is not
+// re-read, and the only halo is one recomputed conv_a row at each segment seam (+1/8 conv_a
+// work at 16-row segments).  LDS rows are 66 pixel records (the image's columns plus zero
+// records for columns -1 and W, conv SAME padding), chunk c of record r in slot c ^ (2r & 15):
+// every B-fragment ds_read_b128 (16 consecutive pixels per lane group) is conflict-free
+// (the GeomWS swizzle, checked for the row layout against MI355X_MICROARCH.md's lane groups).
+// ------------------------------------------------------------------------------------
+constexpr int K3P_MAX_W = 64;
+constexpr int K3P_REC = 256;                        // split record: 64 ch x [hi | lo] f16
+constexpr int K3P_RW = K3P_MAX_W + 2;               // records per LDS row
+constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 16,896 B
+constexpr int K3P_NI = 5, K3P_NC = 4;               // input / conv_a ring rows
+constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 152,064 B
+constexpr int K3P_SR = 16;                          // output rows per block segment
+
+__device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
+
+template <int MT>
+__global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
+  constexpr int COUT = 64, KST = 2;
+  __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
+  char* in_ring = lds;
+  char* c3_ring = lds + K3P_NI * K3P_ROWB;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int role = wave >> 2, w = wave & 3;  // role 0: conv_a, 1: conv_b; w: 16-channel group
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int H = a.H, W = a.W;
+  const int nseg = (H + K3P_SR - 1) / K3P_SR;
+  const int items = a.P * nseg;
+  const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
+
+  // zero records: columns -1 and W.. of every ring row (never written afterwards)
+  for (int q = threadIdx.x; q < (K3P_NI + K3P_NC) * K3P_RW * 16; q += 512) {
+    const int row = q / (K3P_RW * 16), r = q - row * (K3P_RW * 16), rec = r >> 4;
+    if (rec == 0 || rec > W) *(u32x4*)(lds + row * K3P_ROWB + r * 16) = (u32x4){0u, 0u, 0u, 0u};
+  }
+
+  // B fragments: pixel 16 m + l16 of an LDS row at tap column kw -> record 16 m + l16 + kw;
+  // lane group g reads chunk 8 hl + 4 ks + g (the XOR with (2 hl + ks) << 6 selects hl, ks)
+  int bx[3];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) bx[kw] = k3p_off(l16 + kw, g);
+  const int chunk_st = (g & 1) * 8 + 2 * w + (g >> 1);  // this lane's 16-B granule after swap16_pair
+  const int chunk_rh = 2 * w + (g >> 1), rsub = 8 * (g & 1);  // residual: hi / lo of channels 16 w + 4 g ..
+
+  f16x8 wr[9][KST][2];
+  int model = -1;
+  float scale = 0.f;
+  f32x4 bias = {};
+  float rmax = 0.f;
+  auto load_weights = [&](int m) {
+    const uint16_t* wx = role == 0 ? a.wx : a.wx2;
+    constexpr int TAP_BYTES = 64 * COUT * 4;
+    const char* wsrc = (const char*)wx + (size_t)m * 9 * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          wr[t][ks][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
+                                          ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + w * 16 + l16) * 16);
+    scale = role == 0 ? a.wscale[m] : a.wscale2[m];
+    bias = *(const f32x4*)((role == 0 ? a.bias : a.bias2) + m * COUT + 16 * w + 4 * g);
+  };
+
+  // input row y (zeros outside the plane) into ring slot `slot`: W x 16 chunks = ceil(W / 4)
+  // DMA pieces of 1 KB over the 8 waves; LDS slot k of record 1 + x holds chunk k ^ (2 rec & 15)
+  auto dma_row = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int slot) {
+    const int npiece = (W * 16 + 63) / 64;
+    char* dst = in_ring + slot * K3P_ROWB + K3P_REC;
+    for (int k = wave; k < npiece; k += 8) {
+      const int q = 64 * k + lane, x = q >> 4, rec = x + 1, ch = (q & 15) ^ ((2 * rec) & 15);
+      const bool ok = (unsigned)y < (unsigned)H && x < W;
+      dma16_buf(rs, ok ? (unsigned)((y * W + x) * K3P_REC + ch * 16) : kDmaOOR, dst + k * 1024);
+    }
+  };
+
+  // one output row of this wave's layer: taps (kh, kw) over LDS rows r_kh (byte offsets)
+  f32x4 acc[MT];
+  auto conv_row = [&](unsigned r0b, unsigned r1b, unsigned r2b) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    constexpr int NSTEP = 9 * KST;
+    auto frag = [&](int m, int st, int hl) {
+      const int t = st / KST, ks = st - t * KST, kh = t / 3, kw = t - kh * 3;
+      const unsigned rb = kh == 0 ? r0b : kh == 1 ? r1b : r2b;
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(rb + (unsigned)(bx[kw] ^ ((2 * hl + ks) << 6)) +
+                                                                      (unsigned)(m * 16 * K3P_REC)));
+    };
+    f16x8 fb[MT][2];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      fb[m][0] = frag(m, 0, 0);
+      fb[m][1] = frag(m, 0, 1);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      const int t = st / KST, ks = st - t * KST;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
+        if (st + 1 < NSTEP) {
+          fb[m][0] = frag(m, st + 1, 0);
+          fb[m][1] = frag(m, st + 1, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const int p = item / nseg, sg = item - p * nseg;
+    const int r0 = sg * K3P_SR, r1 = min(r0 + K3P_SR, H), nrow = r1 - r0;
+    const int m_item = p >= a.nimg ? 1 : 0;
+    if (m_item != model) {  // wave-uniform: items of one model are consecutive
+      model = m_item;
+      load_weights(model);
+    }
+    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+    // input rows r0 - 2 .. r0 (ring slot of row y: (y - r0 + 2) % 5)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dma_row(rs_in, r0 - 2 + k, k);
+    dma_wait_all();
+    stage_barrier();
+    for (int j = 0; j <= nrow + 2; ++j) {
+      if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);  // lands during this step
+      if (role == 0) {
+        if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
+          const int y3 = r0 - 1 + j;
+          char* dst = c3_ring + (j % K3P_NC) * K3P_ROWB;
+          const bool live = (unsigned)y3 < (unsigned)H;
+          if (live)
+            conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
+                     in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB));
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int x = 16 * m + l16;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (live) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+              if (x < W) range_track(rmax, v);
+            }
+            f16x4 hi, lo;
+            split4(v, hi, lo);
+            const u32x4 q = swap16_pair(hi, lo);  // rows outside the plane: zeros (conv_b's padding)
+            if (x < W) *(u32x4*)(dst + k3p_off(x + 1, chunk_st)) = q;
+          }
+        }
+      } else if (j >= 3) {  // conv_b row y4 = r0 + j - 3 from conv_a rows y4 - 1 .. y4 + 1
+        const int y4 = r0 + j - 3;
+        conv_row(c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB), c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
+                 c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB));
+        const char* res = in_ring + ((j + 4) % K3P_NI) * K3P_ROWB;  // input row y4 (the residual)
+        const unsigned orow = (unsigned)(y4 * W) * K3P_REC + (unsigned)chunk_st * 16;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int x = 16 * m + l16;
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 Hr = *(const u32x2*)(res + k3p_off(x + 1, chunk_rh) + rsub);
+          const u32x2 Lr = *(const u32x2*)(res + k3p_off(x + 1, 8 + chunk_rh) + rsub);
+          f32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+          static_for<4>([&](auto rc) {  // x = x + res (encoder.py:25, decoder.py:29)
+            constexpr int r = decltype(rc)::value;
+            v[r] = __fadd_rn(v[r], add_f16_pair<r & 1>(Hr[r >> 1], Lr[r >> 1]));
+          });
+          if (x < W) range_track(rmax, v);
+          f16x4 hi, lo;
+          split4(v, hi, lo);
+          const u32x4 q = swap16_pair(hi, lo);
+          __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, x < W ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
+        }
+      }
+      dma_wait_all();    // this wave's DMA of the next input row landed
+      lds_reads_done();  // and its LDS reads / conv_a writes are done
+      stage_barrier();
+    }
+  }
+  range_report(a.rg, rmax);
+}
+
+bool k3pair_supported(int H, int W) { return H > 0 && W > 0 && W <= K3P_MAX_W && (long long)H * W * K3P_REC < (1LL << 31); }
+
+// ------------------------------------------------------------------------------------
 // conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
 // utils.py:74-77).  Block: 16x16 output pixels of one plane, 4 waves x 2 M tiles x 32 co.
 // K = 25 taps padded to 26 (13 MFMAs); lane half h supplies tap 2s+h of step s.
@@ -3819,6 +4029,26 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   }
   hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP, PROJ>), dim3(a.ws_blk[a.ws_ngrp]),
                      dim3(64 * (COUT / 16)), 0, st, a);
+  return hipGetLastError();
+}
+
+// The fused k3 residual pair: persistent blocks (one per CU) over (plane, 16-row segment)
+// items, planes in order so a block reloads its weights only when the model changes.
+hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  if (!k3pair_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wx2 || !a.bias2 || a.P != 3 * a.nimg)
+    return hipErrorInvalidValue;
+  const long long items = (long long)a.P * ((a.H + K3P_SR - 1) / K3P_SR);
+  if (items == 0) return hipSuccess;
+  if (items > INT32_MAX) return hipErrorInvalidValue;
+  const int grid = (int)std::min<long long>(items, device_cus());
+  const int mt = (a.W + 15) / 16;
+  switch (mt) {
+    case 1: hipLaunchKernelGGL(conv_k3pair_kernel<1>, dim3(grid), dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(conv_k3pair_kernel<2>, dim3(grid), dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(conv_k3pair_kernel<3>, dim3(grid), dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL(conv_k3pair_kernel<4>, dim3(grid), dim3(512), 0, st, a); break;
+  }
   return hipGetLastError();
 }
 

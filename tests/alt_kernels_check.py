@@ -25,7 +25,8 @@ from test_gpu_parity import PREQUANT_ATOL, check_codes, check_recon  # noqa: E40
 
 def main():
     ws_off = os.environ.get("NIC_WS") == "0"
-    assert ws_off or os.environ.get("NIC_D8") in ("tile", "strip") or os.environ.get("NIC_D8G") == "l"
+    assert (ws_off or os.environ.get("NIC_D8") in ("tile", "strip") or os.environ.get("NIC_D8G") == "l"
+            or os.environ.get("NIC_K3P") == "0")
     c = Codec(0, precision="f16x3")
     c.set_weights(W.seeded_weights(0, init="spread"))
     for case in ("kodim21_256", "imagenet4", "odd37x53"):
@@ -48,11 +49,14 @@ def main():
 
 
 def alt_cases(c):
-    """Decodes compared bit for bit across kernel variants: the golden latents, a random
-    latent whose dconv7 grid has partial 8x8 tiles (odd sizes), and a 3-image 256^2 batch."""
+    """Outputs compared bit for bit across kernel variants: decodes of the golden latents, of
+    random latents whose dconv7 grid has partial 8x8 tiles (odd sizes) and of a 3-image 256^2
+    batch; encodes (codes and fp32 pre-quant latent) of the golden inputs."""
     out = {}
     for case in ("kodim21_256", "imagenet4", "odd37x53"):
-        out[case] = c.decode(torch.from_numpy(load_case(case)["latent"]).cuda())
+        g = load_case(case)
+        out[case] = c.decode(torch.from_numpy(g["latent"]).cuda())
+        out[case + "_z"], out[case + "_f"] = c.encode(torch.from_numpy(g["x"]).cuda(), prequant=True)
     rng = np.random.default_rng(77)
     for i, (h8, w8) in enumerate(((5, 7), (9, 3), (32, 32))):
         z = rng.integers(0, 256, (3, h8, w8, 96), dtype=np.uint8)

@@ -480,10 +480,12 @@ def test_layer_timing(codecs):
         c.decode(c.encode(x))
     t = c.layer_times()
     c.set_timing(False)
-    # f16x3 runs conv1 inside conv2's kernel (no launch of its own); fp32 launches it
+    # f16x3 runs conv1 inside conv2's kernel (no launch of its own), and the k3 residual
+    # pairs of these 16-column planes as one launch each (timed as conv4 / dconv6)
     fused = c.precision == "f16x3"
     assert t["conv1"][1] == (0 if fused else 3)
-    assert all(n == 3 and ms > 0 for name, (ms, n) in t.items() if name != "conv1")
+    assert t["conv3"][1] == t["dconv5"][1] == (0 if fused else 3)
+    assert all(n == 3 and ms > 0 for name, (ms, n) in t.items() if name not in ("conv1", "conv3", "dconv5"))
 
 
 def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden):
@@ -522,8 +524,9 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
             assert (tmp_path / a / f"img{i}.png").read_bytes() == (tmp_path / b / f"img{i}.png").read_bytes()
 
 
-@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"}],
-                         ids=["ws0-tile", "strip", "gather-lds"])
+@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
+                                      {"NIC_K3P": "0"}],
+                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the
@@ -537,9 +540,10 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
-    if switches == {"NIC_D8G": "l"}:
-        # the LDS-staged gather sums the same projections in the same order as the direct one
-        # (bit-identical reconstructions)
+    if switches in ({"NIC_D8G": "l"}, {"NIC_K3P": "0"}):
+        # the LDS-staged gather sums the same projections in the same order as the direct one,
+        # and the fused k3 residual pair runs the same MFMA chains and epilogues as the two
+        # weight-stationary launches: bit-identical outputs
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from alt_kernels_check import alt_cases
 
