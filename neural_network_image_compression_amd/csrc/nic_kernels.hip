@@ -2596,6 +2596,7 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) dma_row(rs_in, r0 - 2 + k, k);
     dma_wait_all();
+    lds_reads_done();  // (first item) the zero records are written
     stage_barrier();
     for (int j = 0; j <= nrow + 2; ++j) {
       if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);  // lands during this step
