@@ -2649,7 +2649,12 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, x < W ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
         }
       }
-      dma_wait_all();    // this wave's DMA of the next input row landed
+      // this wave's DMA of the next input row landed; conv_b's MT output stores, issued after
+      // it, may stay in flight (vector memory operations complete in issue order on gfx9)
+      if (role == 1 && j >= 3)
+        __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
+      else
+        dma_wait_all();
       lds_reads_done();  // and its LDS reads / conv_a writes are done
       stage_barrier();
     }
