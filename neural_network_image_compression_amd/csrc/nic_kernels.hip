@@ -2481,7 +2481,7 @@ constexpr int K3P_SR = 16;                          // output rows per block seg
 
 __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
 
-template <int MT>
+template <int MT, bool IL>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   constexpr int COUT = 64, KST = 2;
   __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
@@ -2542,41 +2542,63 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
     }
   };
 
-  // one output row of this wave's layer: taps (kh, kw) over LDS rows r_kh (byte offsets)
+  // one output row of this wave's layer: taps (kh, kw) over LDS rows r_kh (byte offsets).
+  // IL: the M tiles run in two halves; the epilogue `epi(m)` of each first-half tile is issued
+  // inside the second half's MFMA stream (its VALU and LDS work overlaps the matrix pipe: the
+  // two waves of a SIMD leave a step barrier together, so without this both epilogues would
+  // run with the pipe idle), the second half's epilogues after it.
   f32x4 acc[MT];
-  auto conv_row = [&](unsigned r0b, unsigned r1b, unsigned r2b) {
+  auto conv_row = [&](unsigned r0b, unsigned r1b, unsigned r2b, auto&& epi) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int NSTEP = 9 * KST;
+    constexpr int MA = IL ? MT / 2 : 0;
     auto frag = [&](int m, int st, int hl) {
       const int t = st / KST, ks = st - t * KST, kh = t / 3, kw = t - kh * 3;
       const unsigned rb = kh == 0 ? r0b : kh == 1 ? r1b : r2b;
       return *(const __attribute__((address_space(3))) f16x8*)(lds_at(rb + (unsigned)(bx[kw] ^ ((2 * hl + ks) << 6)) +
                                                                       (unsigned)(m * 16 * K3P_REC)));
     };
-    f16x8 fb[MT][2];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      fb[m][0] = frag(m, 0, 0);
-      fb[m][1] = frag(m, 0, 1);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int st = 0; st < NSTEP; ++st) {
-      const int t = st / KST, ks = st - t * KST;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
-        if (st + 1 < NSTEP) {
-          fb[m][0] = frag(m, st + 1, 0);
-          fb[m][1] = frag(m, st + 1, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+    auto stream = [&](auto mlo_c, auto mhi_c, auto&& inter) {
+      constexpr int ML = decltype(mlo_c)::value, MN = decltype(mhi_c)::value - ML;
+      if constexpr (MN > 0) {
+        f16x8 fb[MN][2];
+        static_for<MN>([&](auto mc) {
+          constexpr int m = decltype(mc)::value;
+          fb[m][0] = frag(ML + m, 0, 0);
+          fb[m][1] = frag(ML + m, 0, 1);
+        });
+        __builtin_amdgcn_s_setprio(1);
+        static_for<NSTEP>([&](auto stc) {
+          constexpr int st = decltype(stc)::value, t = st / KST, ks = st % KST;
+          static_for<MN>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[ML + m], 0, 0, 0);  // w_lo*a_hi
+            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[ML + m], 0, 0, 0);  // w_hi*a_lo
+            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[ML + m], 0, 0, 0);  // w_hi*a_hi
+            if constexpr (st + 1 < NSTEP) {
+              fb[m][0] = frag(ML + m, st + 1, 0);
+              fb[m][1] = frag(ML + m, st + 1, 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+          });
+          inter(stc);
+        });
+        __builtin_amdgcn_s_setprio(0);
       }
-    }
-    __builtin_amdgcn_s_setprio(0);
+    };
+    stream(std::integral_constant<int, 0>{}, std::integral_constant<int, MA>{}, [](auto) {});
+    stream(std::integral_constant<int, MA>{}, std::integral_constant<int, MT>{}, [&](auto stc) {
+      constexpr int st = decltype(stc)::value;
+      static_for<MA>([&](auto mc) {  // first-half tile m's epilogue after second-half step (2m + 1) * 18 / (2 MA)
+        constexpr int m = decltype(mc)::value;
+        if constexpr (st == (2 * m + 1) * NSTEP / (2 * MA)) {
+          epi(m);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+    });
+    static_for<MT - MA>([&](auto mc) { epi(MA + decltype(mc)::value); });
   };
 
   const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
@@ -2604,33 +2626,33 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
         if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
           const int y3 = r0 - 1 + j;
           char* dst = c3_ring + (j % K3P_NC) * K3P_ROWB;
-          const bool live = (unsigned)y3 < (unsigned)H;
-          if (live)
-            conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
-                     in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB));
-#pragma unroll
-          for (int m = 0; m < MT; ++m) {
+          auto epi = [&](int m) {
             const int x = 16 * m + l16;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (live) {
+            f32x4 v;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
-              if (x < W) range_track(rmax, v);
-            }
+            for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+            if (x < W) range_track(rmax, v);
             f16x4 hi, lo;
             split4(v, hi, lo);
-            const u32x4 q = swap16_pair(hi, lo);  // rows outside the plane: zeros (conv_b's padding)
+            const u32x4 q = swap16_pair(hi, lo);
             if (x < W) *(u32x4*)(dst + k3p_off(x + 1, chunk_st)) = q;
+          };
+          if ((unsigned)y3 < (unsigned)H) {
+            conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
+                     in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB), epi);
+          } else {  // rows outside the plane: zeros (conv_b's SAME padding)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+              const int x = 16 * m + l16;
+              if (x < W) *(u32x4*)(dst + k3p_off(x + 1, chunk_st)) = (u32x4){0u, 0u, 0u, 0u};
+            }
           }
         }
       } else if (j >= 3) {  // conv_b row y4 = r0 + j - 3 from conv_a rows y4 - 1 .. y4 + 1
         const int y4 = r0 + j - 3;
-        conv_row(c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB), c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
-                 c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB));
         const char* res = in_ring + ((j + 4) % K3P_NI) * K3P_ROWB;  // input row y4 (the residual)
         const unsigned orow = (unsigned)(y4 * W) * K3P_REC + (unsigned)chunk_st * 16;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
+        auto epi = [&](int m) {
           const int x = 16 * m + l16;
           typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
           const u32x2 Hr = *(const u32x2*)(res + k3p_off(x + 1, chunk_rh) + rsub);
@@ -2647,7 +2669,9 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
           split4(v, hi, lo);
           const u32x4 q = swap16_pair(hi, lo);
           __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, x < W ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
-        }
+        };
+        conv_row(c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB), c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
+                 c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB), epi);
       }
       // this wave's DMA of the next input row landed; conv_b's MT output stores, issued after
       // it, may stay in flight (vector memory operations complete in issue order on gfx9)
@@ -4049,11 +4073,16 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   if (items > INT32_MAX) return hipErrorInvalidValue;
   const int grid = (int)std::min<long long>(items, device_cus());
   const int mt = (a.W + 15) / 16;
+  static const bool il = [] {  // NIC_K3P_IL=0: epilogues after the whole MFMA stream (A/B)
+    const char* e = getenv("NIC_K3P_IL");
+    return !(e && e[0] == '0');
+  }();
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a); };
   switch (mt) {
-    case 1: hipLaunchKernelGGL(conv_k3pair_kernel<1>, dim3(grid), dim3(512), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(conv_k3pair_kernel<2>, dim3(grid), dim3(512), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(conv_k3pair_kernel<3>, dim3(grid), dim3(512), 0, st, a); break;
-    default: hipLaunchKernelGGL(conv_k3pair_kernel<4>, dim3(grid), dim3(512), 0, st, a); break;
+    case 1: il ? go(conv_k3pair_kernel<1, true>) : go(conv_k3pair_kernel<1, false>); break;
+    case 2: il ? go(conv_k3pair_kernel<2, true>) : go(conv_k3pair_kernel<2, false>); break;
+    case 3: il ? go(conv_k3pair_kernel<3, true>) : go(conv_k3pair_kernel<3, false>); break;
+    default: il ? go(conv_k3pair_kernel<4, true>) : go(conv_k3pair_kernel<4, false>); break;
   }
   return hipGetLastError();
 }
