@@ -25,7 +25,8 @@ LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first ma
     (r"dconv8_gather", "dconv8"), (r"conv_ws_kernel<64, 64, 8, 8, false, true", "dconv7"),
     (r"conv_ws_kernel<64, 64, 8, 8, true, false", "k3_resid"), (r"conv_ws_kernel<64, 64, 8, 8, false, false", "k3"),
     (r"<64, 64, 3, 1, false.*true>", "k3_resid"), (r"<64, 64, 3, 1, false.*false>", "k3"),
-    (r"latent_hist", "hist"), (r"hist_entropy", "entropy"),
+    (r"latent_hist", "hist"), (r"hist_entropy", "entropy"), (r"conv_k3pair_kernel", "k3_pair"),
+    (r"colour_split", "colour"), (r"fp32_chain", "fp32_chain"),
 ]
 
 
@@ -75,11 +76,12 @@ def main():
             d["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * med["GRBM_GUI_ACTIVE"] / 8)
         summary[lay] = d
     # the k3 kernels serve conv3/dconv5 and conv4/dconv6
-    for a, b in (("k3", ("conv3", "dconv5")), ("k3_resid", ("conv4", "dconv6"))):
+    # (the fused residual pair k3_pair is timed as conv4 / dconv6 and replaces both)
+    for a, b in (("k3", ("conv3", "dconv5")), ("k3_resid", ("conv4", "dconv6")), ("k3_pair", ("conv4", "dconv6"))):
         if a in summary:
             for x in b:
                 summary[x] = summary[a]
-    out = {"batch": args.batch, "size": args.size, "source": os.path.relpath(args.pmc_dir),
+    out = {"batch": args.batch, "size": args.size, "source": os.path.relpath(args.pmc_dir).replace("gpurun_out", "profiles"),
            "method": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per dispatch, median over dispatches",
            "layers": summary}
     json.dump(out, sys.stdout, indent=1)
