@@ -2456,8 +2456,9 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 // The two separate weight-stationary launches move, per pixel, the input with its tile halo
 // (256 B x 1.56), conv_a's output out and back in with its halo, the residual, and the
 // output: ~1.6 KB per pixel for 147 kFLOP -- at the f16x3 ridge point (833 TFLOP/s / 8 TB/s).
-// Here a block owns whole rows of one plane (planes up to K3P_MAX_W = 64 columns: the 256^2
-// images of BASELINE config 2) and streams down a segment of K3P_SR output rows:
+// Here a block owns whole rows (planes up to K3P_MAX_W = 64 columns: the 256^2 images of
+// BASELINE config 2) -- a contiguous range of the stream of all planes' rows, one block per
+// CU -- and streams down each plane's part of it:
 //   * the input rows arrive by LDS-DMA into a 5-row ring (row y+2 lands while row y+1 is
 //     being convolved), read once from HBM (+2 rows per segment);
 //   * waves 0-3 (conv_a, 16 output channels each, weights resident in VGPRs) convolve input
@@ -2465,8 +2466,8 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 //   * waves 4-7 (conv_b) convolve rows y-3..y-1 of that ring into output row y-2, add the
 //     residual from the input ring (still resident) and store the split row to HBM.
 // One block barrier per row step.  conv_a's row never leaves the chip, the residual is not
-// re-read, and the only halo is one recomputed conv_a row at each segment seam (+1/8 conv_a
-// work at 16-row segments).  LDS rows are 66 pixel records (the image's columns plus zero
+// re-read, and the only halo is one recomputed conv_a row on each side of a range boundary
+// inside a plane (config 2: 48 rows per block, +4 % conv_a work).  LDS rows are 66 pixel records (the image's columns plus zero
 // records for columns -1 and W, conv SAME padding), chunk c of record r in slot c ^ (2r & 15):
 // every B-fragment ds_read_b128 (16 consecutive pixels per lane group) is conflict-free
 // (the GeomWS swizzle, checked for the row layout against MI355X_MICROARCH.md's lane groups).
@@ -2477,7 +2478,7 @@ constexpr int K3P_RW = K3P_MAX_W + 2;               // records per LDS row
 constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 16,896 B
 constexpr int K3P_NI = 5, K3P_NC = 4;               // input / conv_a ring rows
 constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 152,064 B
-constexpr int K3P_SR = 16;                          // output rows per block segment
+constexpr int K3P_SR = 16;                          // least output rows per block
 
 __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
 
@@ -2491,8 +2492,12 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   const int role = wave >> 2, w = wave & 3;  // role 0: conv_a, 1: conv_b; w: 16-channel group
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   const int H = a.H, W = a.W;
-  const int nseg = (H + K3P_SR - 1) / K3P_SR;
-  const int items = a.P * nseg;
+  // this block's contiguous range of output rows in the stream of all planes' rows (p * H + y),
+  // cut into one segment per plane it touches: the ring pipeline fills and drains once per
+  // segment, and only a segment boundary inside a plane recomputes a conv_a row
+  const long long total_rows = (long long)a.P * H;
+  const long long per_block = (total_rows + gridDim.x - 1) / gridDim.x;
+  const long long g0 = (long long)blockIdx.x * per_block, g1 = min(g0 + per_block, total_rows);
   const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
 
   // zero records: columns -1 and W.. of every ring row (never written afterwards)
@@ -2553,11 +2558,20 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int NSTEP = 9 * KST;
     constexpr int MA = IL ? MT / 2 : 0;
+    // per (kh, kw): row base + this lane's record / slot (row bases are multiples of 256 B, so
+    // the (hl, ks) XOR below leaves them intact): one v_xor per fragment read, the M tile in
+    // the ds_read immediate
+    unsigned xb[3][3];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      xb[0][kw] = r0b + (unsigned)bx[kw];
+      xb[1][kw] = r1b + (unsigned)bx[kw];
+      xb[2][kw] = r2b + (unsigned)bx[kw];
+    }
     auto frag = [&](int m, int st, int hl) {
       const int t = st / KST, ks = st - t * KST, kh = t / 3, kw = t - kh * 3;
-      const unsigned rb = kh == 0 ? r0b : kh == 1 ? r1b : r2b;
-      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(rb + (unsigned)(bx[kw] ^ ((2 * hl + ks) << 6)) +
-                                                                      (unsigned)(m * 16 * K3P_REC)));
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(xb[kh][kw] ^ (unsigned)((2 * hl + ks) << 6)) +
+                                                               m * 16 * K3P_REC);
     };
     auto stream = [&](auto mlo_c, auto mhi_c, auto&& inter) {
       constexpr int ML = decltype(mlo_c)::value, MN = decltype(mhi_c)::value - ML;
@@ -2602,9 +2616,10 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   };
 
   const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
-  for (int item = blockIdx.x; item < items; item += gridDim.x) {
-    const int p = item / nseg, sg = item - p * nseg;
-    const int r0 = sg * K3P_SR, r1 = min(r0 + K3P_SR, H), nrow = r1 - r0;
+  for (long long gs = g0; gs < g1;) {
+    const int p = (int)(gs / H);
+    const int r0 = (int)(gs - (long long)p * H), r1 = (int)min((long long)H, g1 - (long long)p * H), nrow = r1 - r0;
+    gs = (long long)p * H + r1;
     const int m_item = p >= a.nimg ? 1 : 0;
     if (m_item != model) {  // wave-uniform: items of one model are consecutive
       model = m_item;
@@ -4062,16 +4077,16 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// The fused k3 residual pair: persistent blocks (one per CU) over (plane, 16-row segment)
-// items, planes in order so a block reloads its weights only when the model changes.
+// The fused k3 residual pair: persistent blocks (one per CU), each a contiguous range of the
+// planes' rows (planes in order, so a block reloads its weights only when the model changes).
 hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (!k3pair_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wx2 || !a.bias2 || a.P != 3 * a.nimg)
     return hipErrorInvalidValue;
-  const long long items = (long long)a.P * ((a.H + K3P_SR - 1) / K3P_SR);
-  if (items == 0) return hipSuccess;
-  if (items > INT32_MAX) return hipErrorInvalidValue;
-  const int grid = (int)std::min<long long>(items, device_cus());
+  const long long rows = (long long)a.P * a.H;
+  if (rows == 0) return hipSuccess;
+  // at least K3P_SR rows per block (fill / drain amortised), at most one block per CU
+  const int grid = (int)std::max(1LL, std::min<long long>((rows + K3P_SR - 1) / K3P_SR, device_cus()));
   const int mt = (a.W + 15) / 16;
   // NIC_K3P_IL=1: first-half epilogues inside the second half's MFMA stream (A/B: 0.300-0.306
   // vs 0.299-0.300 ms for the plain order, same box over 3 rounds -- not the default)
@@ -4162,7 +4177,8 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
 static int dconv1_variant() {
   static const int v = [] {
     const char* e = getenv("NIC_D1");
-    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5 : 0;
+    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5
+                  : e[0] == '8' ? 6 : 0;
   }();
   return v;
 }
@@ -4191,9 +4207,13 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
         case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
         case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_CODES, OUT_SPLIT, false>(a, st);
         case 5: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
+        // NIC_D1=8: the 8x8-tile form on codes (0.0785-0.0789 vs 0.0763-0.0765 ms for the
+        // default, same box)
+        case 6: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
         // default: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
-        // epilogue); NIC_D1=s the split dequantised activations (3 MFMAs, round 2)
-        default: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        // epilogue; NIC_D1=s the split dequantised activations, 3 MFMAs, round 2) on 8x16
+        // coarse tiles, 4 waves
+        default: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
       }
     case L_DCONV5:
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
