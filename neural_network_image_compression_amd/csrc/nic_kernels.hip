@@ -2473,16 +2473,21 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 // (the GeomWS swizzle, checked for the row layout against MI355X_MICROARCH.md's lane groups).
 // ------------------------------------------------------------------------------------
 constexpr int K3P_MAX_W = 64;
+constexpr int K3P_SW = 62;                          // strip mode: output columns per strip
 constexpr int K3P_REC = 256;                        // split record: 64 ch x [hi | lo] f16
-constexpr int K3P_RW = K3P_MAX_W + 2;               // records per LDS row
-constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 16,896 B
+constexpr int K3P_RW = K3P_MAX_W + 4;               // records per LDS row (66 used, whole DMA pieces)
+constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 17,408 B
 constexpr int K3P_NI = 5, K3P_NC = 4;               // input / conv_a ring rows
-constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 152,064 B
+constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 156,672 B
 constexpr int K3P_SR = 16;                          // least output rows per block
 
 __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
 
-template <int MT, bool IL>
+// STRIP (planes wider than 64 columns, MT = 4): the plane is cut into strips of 62 output
+// columns (a.tiles_x of them); per strip the input rows carry 66 columns (2 each side), conv_a
+// computes 64 (the strip's 62 plus the column either side conv_b needs, zeros outside the
+// plane) and conv_b the strip's 62 (3 % of its lanes and 3 % of conv_a's work are the seams).
+template <int MT, bool IL, bool STRIP>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   constexpr int COUT = 64, KST = 2;
   __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
@@ -2495,7 +2500,9 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   // this block's contiguous range of output rows in the stream of all planes' rows (p * H + y),
   // cut into one segment per plane it touches: the ring pipeline fills and drains once per
   // segment, and only a segment boundary inside a plane recomputes a conv_a row
-  const long long total_rows = (long long)a.P * H;
+  static_assert(!STRIP || MT == 4, "strips are 4 M tiles wide");
+  const int nstrips = STRIP ? a.tiles_x : 1;
+  const long long total_rows = (long long)a.P * nstrips * H;
   const long long per_block = (total_rows + gridDim.x - 1) / gridDim.x;
   const long long g0 = (long long)blockIdx.x * per_block, g1 = min(g0 + per_block, total_rows);
   const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
@@ -2535,14 +2542,21 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
     bias = *(const f32x4*)((role == 0 ? a.bias : a.bias2) + m * COUT + 16 * w + 4 * g);
   };
 
-  // input row y (zeros outside the plane) into ring slot `slot`: W x 16 chunks = ceil(W / 4)
-  // DMA pieces of 1 KB over the 8 waves; LDS slot k of record 1 + x holds chunk k ^ (2 rec & 15)
+  // Column geometry of a segment (strip origin sx0): input record r holds column xi0 + r,
+  // conv_a's pixel i is column xa0 + i (its output record i + ca_off), conv_b's pixel j column
+  // sx0 + j (valid below jmax), whose residual is input record j + rb_off.
+  constexpr int ca_off = STRIP ? 0 : 1, rb_off = STRIP ? 2 : 1, jmax = STRIP ? K3P_SW : 64;
+  constexpr int rec0 = STRIP ? 0 : 1;  // first DMA'd input record (single strip: record 0 is column -1, zero)
+  int sx0 = 0;
+  // input row y (zeros outside the plane) into ring slot `slot`: 1-KB DMA pieces over the 8
+  // waves; LDS slot k of record rec holds chunk k ^ (2 rec & 15) of column xi0 + rec
   auto dma_row = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int slot) {
-    const int npiece = (W * 16 + 63) / 64;
-    char* dst = in_ring + slot * K3P_ROWB + K3P_REC;
+    const int npiece = STRIP ? K3P_RW / 4 : (W * 16 + 63) / 64;
+    const int xi0 = STRIP ? sx0 - 2 : -1;
+    char* dst = in_ring + slot * K3P_ROWB + rec0 * K3P_REC;
     for (int k = wave; k < npiece; k += 8) {
-      const int q = 64 * k + lane, x = q >> 4, rec = x + 1, ch = (q & 15) ^ ((2 * rec) & 15);
-      const bool ok = (unsigned)y < (unsigned)H && x < W;
+      const int q = 64 * k + lane, rec = rec0 + (q >> 4), x = xi0 + rec, ch = (q & 15) ^ ((2 * rec) & 15);
+      const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && rec < K3P_MAX_W + 2;
       dma16_buf(rs, ok ? (unsigned)((y * W + x) * K3P_REC + ch * 16) : kDmaOOR, dst + k * 1024);
     }
   };
@@ -2617,9 +2631,11 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
 
   const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
   for (long long gs = g0; gs < g1;) {
-    const int p = (int)(gs / H);
-    const int r0 = (int)(gs - (long long)p * H), r1 = (int)min((long long)H, g1 - (long long)p * H), nrow = r1 - r0;
-    gs = (long long)p * H + r1;
+    const long long col = gs / H;  // (plane, strip) column of rows
+    const int p = (int)(col / nstrips);
+    sx0 = (int)(col - (long long)p * nstrips) * K3P_SW;
+    const int r0 = (int)(gs - col * H), r1 = (int)min((long long)H, g1 - col * H), nrow = r1 - r0;
+    gs = col * H + r1;
     const int m_item = p >= a.nimg ? 1 : 0;
     if (m_item != model) {  // wave-uniform: items of one model are consecutive
       model = m_item;
@@ -2641,26 +2657,25 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
         if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
           const int y3 = r0 - 1 + j;
           char* dst = c3_ring + (j % K3P_NC) * K3P_ROWB;
+          const int xa0 = STRIP ? sx0 - 1 : 0;
           auto epi = [&](int m) {
-            const int x = 16 * m + l16;
+            const int i = 16 * m + l16, x = xa0 + i;
+            const bool in = (unsigned)x < (unsigned)W;  // outside the plane: zero (conv_b's padding)
             f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
-            if (x < W) range_track(rmax, v);
+            for (int r = 0; r < 4; ++r) v[r] = in ? leaky02(scale_bias(acc[m][r], scale, bias[r])) : 0.f;
+            if (in) range_track(rmax, v);
             f16x4 hi, lo;
             split4(v, hi, lo);
             const u32x4 q = swap16_pair(hi, lo);
-            if (x < W) *(u32x4*)(dst + k3p_off(x + 1, chunk_st)) = q;
+            *(u32x4*)(dst + k3p_off(i + ca_off, chunk_st)) = q;
           };
           if ((unsigned)y3 < (unsigned)H) {
             conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
                      in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB), epi);
           } else {  // rows outside the plane: zeros (conv_b's SAME padding)
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-              const int x = 16 * m + l16;
-              if (x < W) *(u32x4*)(dst + k3p_off(x + 1, chunk_st)) = (u32x4){0u, 0u, 0u, 0u};
-            }
+            for (int m = 0; m < MT; ++m) *(u32x4*)(dst + k3p_off(16 * m + l16 + ca_off, chunk_st)) = (u32x4){0u, 0u, 0u, 0u};
           }
         }
       } else if (j >= 3) {  // conv_b row y4 = r0 + j - 3 from conv_a rows y4 - 1 .. y4 + 1
@@ -2668,10 +2683,11 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
         const char* res = in_ring + ((j + 4) % K3P_NI) * K3P_ROWB;  // input row y4 (the residual)
         const unsigned orow = (unsigned)(y4 * W) * K3P_REC + (unsigned)chunk_st * 16;
         auto epi = [&](int m) {
-          const int x = 16 * m + l16;
+          const int jx = 16 * m + l16, x = sx0 + jx;
+          const bool valid = jx < jmax && x < W;
           typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 Hr = *(const u32x2*)(res + k3p_off(x + 1, chunk_rh) + rsub);
-          const u32x2 Lr = *(const u32x2*)(res + k3p_off(x + 1, 8 + chunk_rh) + rsub);
+          const u32x2 Hr = *(const u32x2*)(res + k3p_off(jx + rb_off, chunk_rh) + rsub);
+          const u32x2 Lr = *(const u32x2*)(res + k3p_off(jx + rb_off, 8 + chunk_rh) + rsub);
           f32x4 v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
@@ -2679,11 +2695,11 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
             constexpr int r = decltype(rc)::value;
             v[r] = __fadd_rn(v[r], add_f16_pair<r & 1>(Hr[r >> 1], Lr[r >> 1]));
           });
-          if (x < W) range_track(rmax, v);
+          if (valid) range_track(rmax, v);
           f16x4 hi, lo;
           split4(v, hi, lo);
           const u32x4 q = swap16_pair(hi, lo);
-          __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, x < W ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, valid ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
         };
         conv_row(c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB), c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
                  c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB), epi);
@@ -2701,7 +2717,16 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   range_report(a.rg, rmax);
 }
 
-bool k3pair_supported(int H, int W) { return H > 0 && W > 0 && W <= K3P_MAX_W && (long long)H * W * K3P_REC < (1LL << 31); }
+// strips for a plane of W columns (0: the fused pair does not take it): one for W <= 64, else
+// 62-column strips when their lanes waste at most 10 % (4K frames: 16 strips over 960 columns)
+static int k3pair_strips(int W) {
+  if (W <= K3P_MAX_W) return 1;
+  const int n = (W + K3P_SW - 1) / K3P_SW;
+  return 10LL * n * 64 <= 11LL * W ? n : 0;
+}
+bool k3pair_supported(int H, int W) {
+  return H > 0 && W > 0 && k3pair_strips(W) > 0 && (long long)H * W * K3P_REC < (1LL << 31);
+}
 
 // ------------------------------------------------------------------------------------
 // conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
@@ -4083,23 +4108,29 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (!k3pair_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wx2 || !a.bias2 || a.P != 3 * a.nimg)
     return hipErrorInvalidValue;
-  const long long rows = (long long)a.P * a.H;
+  a.tiles_x = k3pair_strips(a.W);
+  const long long rows = (long long)a.P * a.tiles_x * a.H;
   if (rows == 0) return hipSuccess;
   // at least K3P_SR rows per block (fill / drain amortised), at most one block per CU
   const int grid = (int)std::max(1LL, std::min<long long>((rows + K3P_SR - 1) / K3P_SR, device_cus()));
   const int mt = (a.W + 15) / 16;
   // NIC_K3P_IL=1: first-half epilogues inside the second half's MFMA stream (A/B: 0.300-0.306
-  // vs 0.299-0.300 ms for the plain order, same box over 3 rounds -- not the default)
+  // vs 0.299-0.300 ms for the plain order, same box over 3 rounds -- not the default; single
+  // strip, MT 4 only)
   static const bool il = [] {
     const char* e = getenv("NIC_K3P_IL");
     return e && e[0] == '1';
   }();
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a); };
-  switch (mt) {
-    case 1: il ? go(conv_k3pair_kernel<1, true>) : go(conv_k3pair_kernel<1, false>); break;
-    case 2: il ? go(conv_k3pair_kernel<2, true>) : go(conv_k3pair_kernel<2, false>); break;
-    case 3: il ? go(conv_k3pair_kernel<3, true>) : go(conv_k3pair_kernel<3, false>); break;
-    default: il ? go(conv_k3pair_kernel<4, true>) : go(conv_k3pair_kernel<4, false>); break;
+  if (a.tiles_x > 1) {
+    go(conv_k3pair_kernel<4, false, true>);
+  } else {
+    switch (mt) {
+      case 1: go(conv_k3pair_kernel<1, false, false>); break;
+      case 2: go(conv_k3pair_kernel<2, false, false>); break;
+      case 3: go(conv_k3pair_kernel<3, false, false>); break;
+      default: il ? go(conv_k3pair_kernel<4, true, false>) : go(conv_k3pair_kernel<4, false, false>); break;
+    }
   }
   return hipGetLastError();
 }

@@ -58,9 +58,12 @@ def alt_cases(c):
         out[case] = c.decode(torch.from_numpy(g["latent"]).cuda())
         out[case + "_z"], out[case + "_f"] = c.encode(torch.from_numpy(g["x"]).cuda(), prequant=True)
     rng = np.random.default_rng(77)
-    for i, (h8, w8) in enumerate(((5, 7), (9, 3), (32, 32))):
-        z = rng.integers(0, 256, (3, h8, w8, 96), dtype=np.uint8)
+    for i, (h8, w8) in enumerate(((5, 7), (9, 3), (32, 32), (8, 300))):
+        z = rng.integers(0, 256, (3 if w8 < 100 else 1, h8, w8, 96), dtype=np.uint8)
         out[f"rand{i}"] = c.decode(torch.from_numpy(z).cuda())
+    # a 64 x 2400 image: its 600-column k3 planes run the fused residual pair in 62-column strips
+    x = rng.integers(0, 256, (1, 64, 2400, 3), dtype=np.uint8)
+    out["wide_z"], out["wide_f"] = c.encode(torch.from_numpy(x).cuda(), prequant=True)
     torch.cuda.synchronize()
     return out
 
