@@ -2567,7 +2567,15 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   // two waves of a SIMD leave a step barrier together, so without this both epilogues would
   // run with the pipe idle), the second half's epilogues after it.
   f32x4 acc[MT];
+#ifdef NIC_STAMPS  // tools/k3p_stamps.cpp: per role, cycles waiting at the step barrier, in the
+                   // MFMA stream, in the epilogue, and in the DMA issue
+  unsigned long long s_wait = 0, s_mfma = 0, s_epi = 0, s_dma = 0, s_t0, s_t1, s_steps = 0;
+  const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
+#endif
   auto conv_row = [&](unsigned r0b, unsigned r1b, unsigned r2b, auto&& epi) {
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t0);
+#endif
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int NSTEP = 9 * KST;
@@ -2626,7 +2634,15 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
         }
       });
     });
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t1);
+    s_mfma += s_t1 - s_t0;
+#endif
     static_for<MT - MA>([&](auto mc) { epi(MA + decltype(mc)::value); });
+#ifdef NIC_STAMPS
+    NIC_PNOW(s_t0);
+    s_epi += s_t0 - s_t1;
+#endif
   };
 
   const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
@@ -2652,7 +2668,16 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
     lds_reads_done();  // (first item) the zero records are written
     stage_barrier();
     for (int j = 0; j <= nrow + 2; ++j) {
+#ifdef NIC_STAMPS
+      unsigned long long s_a, s_b;
+      NIC_PNOW(s_a);
+#endif
       if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);  // lands during this step
+#ifdef NIC_STAMPS
+      NIC_PNOW(s_b);
+      s_dma += s_b - s_a;
+      ++s_steps;
+#endif
       if (role == 0) {
         if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
           const int y3 = r0 - 1 + j;
@@ -2706,15 +2731,35 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
       }
       // this wave's DMA of the next input row landed; conv_b's MT output stores, issued after
       // it, may stay in flight (vector memory operations complete in issue order on gfx9)
+#ifdef NIC_STAMPS
+      NIC_PNOW(s_a);
+#endif
       if (role == 1 && j >= 3)
         __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
       else
         dma_wait_all();
       lds_reads_done();  // and its LDS reads / conv_a writes are done
       stage_barrier();
+#ifdef NIC_STAMPS
+      NIC_PNOW(s_b);
+      s_wait += s_b - s_a;
+#endif
     }
   }
   range_report(a.rg, rmax);
+#ifdef NIC_STAMPS
+  if (lane == 0 && (wave == 0 || wave == 4)) {
+    unsigned long long* o = g_stamps + (size_t)blockIdx.x * 16 + role * 8;
+    o[0] = s_wait;
+    o[1] = s_mfma;
+    o[2] = s_epi;
+    o[3] = s_dma;
+    o[4] = s_steps;
+    o[5] = __builtin_amdgcn_s_memtime() - s_c0;
+    o[6] = __builtin_amdgcn_s_memrealtime() - s_rt0;
+    o[7] = 1;
+  }
+#endif
 }
 
 // strips for a plane of W columns (0: the fused pair does not take it): one for W <= 64, else
