@@ -2487,7 +2487,7 @@ __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_RE
 // columns (a.tiles_x of them); per strip the input rows carry 66 columns (2 each side), conv_a
 // computes 64 (the strip's 62 plus the column either side conv_b needs, zeros outside the
 // plane) and conv_b the strip's 62 (3 % of its lanes and 3 % of conv_a's work are the seams).
-template <int MT, bool IL, bool STRIP>
+template <int MT, bool SKEW, bool STRIP>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   constexpr int COUT = 64, KST = 2;
   __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
@@ -2550,22 +2550,21 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   int sx0 = 0;
   // input row y (zeros outside the plane) into ring slot `slot`: 1-KB DMA pieces over the 8
   // waves; LDS slot k of record rec holds chunk k ^ (2 rec & 15) of column xi0 + rec
+  // SKEW: the conv_a waves issue every piece (conv_b's step then starts with its epilogue)
   auto dma_row = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int slot) {
     const int npiece = STRIP ? K3P_RW / 4 : (W * 16 + 63) / 64;
     const int xi0 = STRIP ? sx0 - 2 : -1;
     char* dst = in_ring + slot * K3P_ROWB + rec0 * K3P_REC;
-    for (int k = wave; k < npiece; k += 8) {
+    if (SKEW && role) return;
+    for (int k = SKEW ? w : wave; k < npiece; k += SKEW ? 4 : 8) {
       const int q = 64 * k + lane, rec = rec0 + (q >> 4), x = xi0 + rec, ch = (q & 15) ^ ((2 * rec) & 15);
       const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && rec < K3P_MAX_W + 2;
       dma16_buf(rs, ok ? (unsigned)((y * W + x) * K3P_REC + ch * 16) : kDmaOOR, dst + k * 1024);
     }
   };
 
-  // one output row of this wave's layer: taps (kh, kw) over LDS rows r_kh (byte offsets).
-  // IL: the M tiles run in two halves; the epilogue `epi(m)` of each first-half tile is issued
-  // inside the second half's MFMA stream (its VALU and LDS work overlaps the matrix pipe: the
-  // two waves of a SIMD leave a step barrier together, so without this both epilogues would
-  // run with the pipe idle), the second half's epilogues after it.
+  // one output row of this wave's layer: taps (kh, kw) over LDS rows r_kh (byte offsets), then
+  // `epi(m)` for each M tile (a no-op for conv_b in SKEW mode: its epilogue runs next step)
   f32x4 acc[MT];
 #ifdef NIC_STAMPS  // tools/k3p_stamps.cpp: per role, cycles waiting at the step barrier, in the
                    // MFMA stream, in the epilogue, and in the DMA issue
@@ -2579,7 +2578,6 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int NSTEP = 9 * KST;
-    constexpr int MA = IL ? MT / 2 : 0;
     // per (kh, kw): row base + this lane's record / slot (row bases are multiples of 256 B, so
     // the (hl, ks) XOR below leaves them intact): one v_xor per fragment read, the M tile in
     // the ds_read immediate
@@ -2595,50 +2593,33 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
       return *(const __attribute__((address_space(3))) f16x8*)(lds_at(xb[kh][kw] ^ (unsigned)((2 * hl + ks) << 6)) +
                                                                m * 16 * K3P_REC);
     };
-    auto stream = [&](auto mlo_c, auto mhi_c, auto&& inter) {
-      constexpr int ML = decltype(mlo_c)::value, MN = decltype(mhi_c)::value - ML;
-      if constexpr (MN > 0) {
-        f16x8 fb[MN][2];
-        static_for<MN>([&](auto mc) {
-          constexpr int m = decltype(mc)::value;
-          fb[m][0] = frag(ML + m, 0, 0);
-          fb[m][1] = frag(ML + m, 0, 1);
-        });
-        __builtin_amdgcn_s_setprio(1);
-        static_for<NSTEP>([&](auto stc) {
-          constexpr int st = decltype(stc)::value, t = st / KST, ks = st % KST;
-          static_for<MN>([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[ML + m], 0, 0, 0);  // w_lo*a_hi
-            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[ML + m], 0, 0, 0);  // w_hi*a_lo
-            acc[ML + m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[ML + m], 0, 0, 0);  // w_hi*a_hi
-            if constexpr (st + 1 < NSTEP) {
-              fb[m][0] = frag(ML + m, st + 1, 0);
-              fb[m][1] = frag(ML + m, st + 1, 1);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
-          });
-          inter(stc);
-        });
-        __builtin_amdgcn_s_setprio(0);
-      }
-    };
-    stream(std::integral_constant<int, 0>{}, std::integral_constant<int, MA>{}, [](auto) {});
-    stream(std::integral_constant<int, MA>{}, std::integral_constant<int, MT>{}, [&](auto stc) {
-      constexpr int st = decltype(stc)::value;
-      static_for<MA>([&](auto mc) {  // first-half tile m's epilogue after second-half step (2m + 1) * 18 / (2 MA)
+    f16x8 fb[MT][2];
+    static_for<MT>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      fb[m][0] = frag(m, 0, 0);
+      fb[m][1] = frag(m, 0, 1);
+    });
+    __builtin_amdgcn_s_setprio(1);
+    static_for<NSTEP>([&](auto stc) {
+      constexpr int st = decltype(stc)::value, t = st / KST, ks = st % KST;
+      static_for<MT>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        if constexpr (st == (2 * m + 1) * NSTEP / (2 * MA)) {
-          epi(m);
-          __builtin_amdgcn_sched_barrier(0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
+        if constexpr (st + 1 < NSTEP) {
+          fb[m][0] = frag(m, st + 1, 0);
+          fb[m][1] = frag(m, st + 1, 1);
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
       });
     });
+    __builtin_amdgcn_s_setprio(0);
 #ifdef NIC_STAMPS
     NIC_PNOW(s_t1);
     s_mfma += s_t1 - s_t0;
 #endif
-    static_for<MT - MA>([&](auto mc) { epi(MA + decltype(mc)::value); });
+    static_for<MT>([&](auto mc) { epi(decltype(mc)::value); });
 #ifdef NIC_STAMPS
     NIC_PNOW(s_t0);
     s_epi += s_t0 - s_t1;
@@ -2646,106 +2627,151 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   };
 
   const unsigned in_base = lds_off(in_ring), c3_base = lds_off(c3_ring);
-  for (long long gs = g0; gs < g1;) {
-    const long long col = gs / H;  // (plane, strip) column of rows
-    const int p = (int)(col / nstrips);
-    sx0 = (int)(col - (long long)p * nstrips) * K3P_SW;
-    const int r0 = (int)(gs - col * H), r1 = (int)min((long long)H, g1 - col * H), nrow = r1 - r0;
-    gs = col * H + r1;
-    const int m_item = p >= a.nimg ? 1 : 0;
-    if (m_item != model) {  // wave-uniform: items of one model are consecutive
-      model = m_item;
-      load_weights(model);
+  // conv_b: the residual (input row y4, split) of this lane's 4 channels per M tile, read from
+  // the input ring into registers; epilogue of output row y4 from acc and those registers
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 rr[MT][2];
+  auto load_res = [&](const char* res) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int jx = 16 * m + l16;
+      rr[m][0] = *(const u32x2*)(res + k3p_off(jx + rb_off, chunk_rh) + rsub);
+      rr[m][1] = *(const u32x2*)(res + k3p_off(jx + rb_off, 8 + chunk_rh) + rsub);
     }
-    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
-    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
-    // input rows r0 - 2 .. r0 (ring slot of row y: (y - r0 + 2) % 5)
+  };
+  auto epi_b = [&](int m, int y4, const __amdgpu_buffer_rsrc_t& rs_out) {
+    const int jx = 16 * m + l16, x = sx0 + jx;
+    const bool valid = jx < jmax && x < W;
+    f32x4 v;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) dma_row(rs_in, r0 - 2 + k, k);
-    dma_wait_all();
-    lds_reads_done();  // (first item) the zero records are written
-    stage_barrier();
-    for (int j = 0; j <= nrow + 2; ++j) {
+    for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+    static_for<4>([&](auto rc) {  // x = x + res (encoder.py:25, decoder.py:29)
+      constexpr int r = decltype(rc)::value;
+      v[r] = __fadd_rn(v[r], add_f16_pair<r & 1>(rr[m][0][r >> 1], rr[m][1][r >> 1]));
+    });
+    if (valid) range_track(rmax, v);
+    f16x4 hi, lo;
+    split4(v, hi, lo);
+    const u32x4 q = swap16_pair(hi, lo);
+    const unsigned orow = (unsigned)(y4 * W) * K3P_REC + (unsigned)chunk_st * 16;
+    __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, valid ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
+  };
+  // the step loop per role, compiled separately: values one role keeps across the step
+  // barrier (conv_b's accumulators and residual in SKEW mode) are not live in the other's code
+  auto run = [&](auto role_c) {
+    constexpr int ROLE = decltype(role_c)::value;
+    for (long long gs = g0; gs < g1;) {
+      const long long col = gs / H;  // (plane, strip) column of rows
+      const int p = (int)(col / nstrips);
+      sx0 = (int)(col - (long long)p * nstrips) * K3P_SW;
+      const int r0 = (int)(gs - col * H), r1 = (int)min((long long)H, g1 - col * H), nrow = r1 - r0;
+      gs = col * H + r1;
+      const int m_item = p >= a.nimg ? 1 : 0;
+      if (m_item != model) {  // wave-uniform: items of one model are consecutive
+        model = m_item;
+        load_weights(model);
+      }
+      const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+      const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+      // input rows r0 - 2 .. r0 (ring slot of row y: (y - r0 + 2) % 5)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dma_row(rs_in, r0 - 2 + k, k);
+      dma_wait_all();
+      lds_reads_done();  // (first item) the zero records are written
+      stage_barrier();
+      for (int j = 0; j <= nrow + 2; ++j) {
 #ifdef NIC_STAMPS
-      unsigned long long s_a, s_b;
-      NIC_PNOW(s_a);
+        unsigned long long s_a, s_b;
+        NIC_PNOW(s_a);
 #endif
-      if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);  // lands during this step
+        // the next input row lands during this step.  (SKEW: issuing conv_a's pieces inside its
+        // MFMA stream instead measured no faster -- 4 LDS-DMA issues cost ~700 cycles either way)
+        if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);
 #ifdef NIC_STAMPS
-      NIC_PNOW(s_b);
-      s_dma += s_b - s_a;
-      ++s_steps;
+        NIC_PNOW(s_b);
+        s_dma += s_b - s_a;
+        ++s_steps;
 #endif
-      if (role == 0) {
-        if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
-          const int y3 = r0 - 1 + j;
-          char* dst = c3_ring + (j % K3P_NC) * K3P_ROWB;
-          const int xa0 = STRIP ? sx0 - 1 : 0;
-          auto epi = [&](int m) {
-            const int i = 16 * m + l16, x = xa0 + i;
-            const bool in = (unsigned)x < (unsigned)W;  // outside the plane: zero (conv_b's padding)
-            f32x4 v;
+        if constexpr (ROLE == 0) {
+          if (j <= nrow + 1) {  // conv_a row y3 = r0 - 1 + j into conv_a ring slot j % 4
+            const int y3 = r0 - 1 + j;
+            char* dst = c3_ring + (j % K3P_NC) * K3P_ROWB;
+            const int xa0 = STRIP ? sx0 - 1 : 0;
+            auto epi = [&](int m) {
+              const int i = 16 * m + l16, x = xa0 + i;
+              const bool in = (unsigned)x < (unsigned)W;  // outside the plane: zero (conv_b's padding)
+              f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = in ? leaky02(scale_bias(acc[m][r], scale, bias[r])) : 0.f;
-            if (in) range_track(rmax, v);
-            f16x4 hi, lo;
-            split4(v, hi, lo);
-            const u32x4 q = swap16_pair(hi, lo);
-            *(u32x4*)(dst + k3p_off(i + ca_off, chunk_st)) = q;
-          };
-          if ((unsigned)y3 < (unsigned)H) {
-            conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
-                     in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB), epi);
-          } else {  // rows outside the plane: zeros (conv_b's SAME padding)
+              for (int r = 0; r < 4; ++r) v[r] = in ? leaky02(scale_bias(acc[m][r], scale, bias[r])) : 0.f;
+              if (in) range_track(rmax, v);
+              f16x4 hi, lo;
+              split4(v, hi, lo);
+              const u32x4 q = swap16_pair(hi, lo);
+              *(u32x4*)(dst + k3p_off(i + ca_off, chunk_st)) = q;
+            };
+            if ((unsigned)y3 < (unsigned)H) {
+              conv_row(in_base + (unsigned)((j % K3P_NI) * K3P_ROWB), in_base + (unsigned)(((j + 1) % K3P_NI) * K3P_ROWB),
+                       in_base + (unsigned)(((j + 2) % K3P_NI) * K3P_ROWB), epi);
+            } else {  // rows outside the plane: zeros (conv_b's SAME padding)
 #pragma unroll
-            for (int m = 0; m < MT; ++m) *(u32x4*)(dst + k3p_off(16 * m + l16 + ca_off, chunk_st)) = (u32x4){0u, 0u, 0u, 0u};
+              for (int m = 0; m < MT; ++m) *(u32x4*)(dst + k3p_off(16 * m + l16 + ca_off, chunk_st)) = (u32x4){0u, 0u, 0u, 0u};
+            }
+          }
+        } else if (j >= 3) {  // conv_b row y4 = r0 + j - 3 from conv_a rows y4 - 1 .. y4 + 1
+          const int y4 = r0 + j - 3;
+          const char* res = in_ring + ((j + 4) % K3P_NI) * K3P_ROWB;  // input row y4 (the residual)
+          const unsigned cb0 = c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB),
+                         cb1 = c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
+                         cb2 = c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB);
+          if constexpr (SKEW) {
+            if (j >= 4) {  // row y4 - 1: its accumulators and residual are still in registers
+#ifdef NIC_STAMPS
+              unsigned long long s_e0, s_e1;
+              NIC_PNOW(s_e0);
+#endif
+              static_for<MT>([&](auto mc) { epi_b(decltype(mc)::value, y4 - 1, rs_out); });
+#ifdef NIC_STAMPS
+              NIC_PNOW(s_e1);
+              s_epi += s_e1 - s_e0;
+#endif
+            }
+            conv_row(cb0, cb1, cb2, [](int) {});
+            load_res(res);  // row y4's residual, read before the next step's DMA reuses its slot
+          } else {
+            conv_row(cb0, cb1, cb2, [&](int m) {
+              if (m == 0) load_res(res);
+              epi_b(m, y4, rs_out);
+            });
           }
         }
-      } else if (j >= 3) {  // conv_b row y4 = r0 + j - 3 from conv_a rows y4 - 1 .. y4 + 1
-        const int y4 = r0 + j - 3;
-        const char* res = in_ring + ((j + 4) % K3P_NI) * K3P_ROWB;  // input row y4 (the residual)
-        const unsigned orow = (unsigned)(y4 * W) * K3P_REC + (unsigned)chunk_st * 16;
-        auto epi = [&](int m) {
-          const int jx = 16 * m + l16, x = sx0 + jx;
-          const bool valid = jx < jmax && x < W;
-          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 Hr = *(const u32x2*)(res + k3p_off(jx + rb_off, chunk_rh) + rsub);
-          const u32x2 Lr = *(const u32x2*)(res + k3p_off(jx + rb_off, 8 + chunk_rh) + rsub);
-          f32x4 v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
-          static_for<4>([&](auto rc) {  // x = x + res (encoder.py:25, decoder.py:29)
-            constexpr int r = decltype(rc)::value;
-            v[r] = __fadd_rn(v[r], add_f16_pair<r & 1>(Hr[r >> 1], Lr[r >> 1]));
-          });
-          if (valid) range_track(rmax, v);
-          f16x4 hi, lo;
-          split4(v, hi, lo);
-          const u32x4 q = swap16_pair(hi, lo);
-          __builtin_amdgcn_raw_buffer_store_b128(q, rs_out, valid ? orow + (unsigned)(x * K3P_REC) : kDmaOOR, 0, 0);
-        };
-        conv_row(c3_base + (unsigned)(((j + 1) % K3P_NC) * K3P_ROWB), c3_base + (unsigned)(((j + 2) % K3P_NC) * K3P_ROWB),
-                 c3_base + (unsigned)(((j + 3) % K3P_NC) * K3P_ROWB), epi);
+        // this wave's DMA of the next input row landed; conv_b's MT output stores, issued after
+        // it, may stay in flight (vector memory operations complete in issue order on gfx9).
+        // SKEW: conv_b issues no DMA -- only its LDS reads must be done
+#ifdef NIC_STAMPS
+        NIC_PNOW(s_a);
+#endif
+        if (ROLE == 1 && (SKEW || j >= 3)) {
+          if constexpr (!SKEW) __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
+        } else {
+          dma_wait_all();
+        }
+        lds_reads_done();  // and its LDS reads / conv_a writes are done
+        stage_barrier();
+#ifdef NIC_STAMPS
+        NIC_PNOW(s_b);
+        s_wait += s_b - s_a;
+#endif
       }
-      // this wave's DMA of the next input row landed; conv_b's MT output stores, issued after
-      // it, may stay in flight (vector memory operations complete in issue order on gfx9)
-#ifdef NIC_STAMPS
-      NIC_PNOW(s_a);
-#endif
-      if (role == 1 && j >= 3)
-        __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
-      else
-        dma_wait_all();
-      lds_reads_done();  // and its LDS reads / conv_a writes are done
-      stage_barrier();
-#ifdef NIC_STAMPS
-      NIC_PNOW(s_b);
-      s_wait += s_b - s_a;
-#endif
+      if constexpr (SKEW)  // the segment's last conv_b row
+        if (ROLE == 1 && nrow > 0) static_for<MT>([&](auto mc) { epi_b(decltype(mc)::value, r0 + nrow - 1, rs_out); });
     }
-  }
+  };
+  if (role == 0)
+    run(std::integral_constant<int, 0>{});
+  else
+    run(std::integral_constant<int, 1>{});
   range_report(a.rg, rmax);
 #ifdef NIC_STAMPS
   if (lane == 0 && (wave == 0 || wave == 4)) {
@@ -4159,24 +4185,27 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   // at least K3P_SR rows per block (fill / drain amortised), at most one block per CU
   const int grid = (int)std::max(1LL, std::min<long long>((rows + K3P_SR - 1) / K3P_SR, device_cus()));
   const int mt = (a.W + 15) / 16;
-  // NIC_K3P_IL=1: first-half epilogues inside the second half's MFMA stream (A/B: 0.300-0.306
-  // vs 0.299-0.300 ms for the plain order, same box over 3 rounds -- not the default; single
-  // strip, MT 4 only)
-  static const bool il = [] {
-    const char* e = getenv("NIC_K3P_IL");
-    return e && e[0] == '1';
+  // SKEW (default; NIC_K3P_SK=0 for the lockstep order): conv_b runs each row's epilogue at the
+  // start of the next step, beside conv_a's MFMA stream, instead of after its own stream
+  static const bool sk = [] {
+    const char* e = getenv("NIC_K3P_SK");
+    return !(e && e[0] == '0');
   }();
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a); };
-  if (a.tiles_x > 1) {
-    go(conv_k3pair_kernel<4, false, true>);
-  } else {
-    switch (mt) {
-      case 1: go(conv_k3pair_kernel<1, false, false>); break;
-      case 2: go(conv_k3pair_kernel<2, false, false>); break;
-      case 3: go(conv_k3pair_kernel<3, false, false>); break;
-      default: il ? go(conv_k3pair_kernel<4, true, false>) : go(conv_k3pair_kernel<4, false, false>); break;
+  auto pick = [&](auto skc) {
+    constexpr bool SK = decltype(skc)::value;
+    if (a.tiles_x > 1) {
+      go(conv_k3pair_kernel<4, SK, true>);
+    } else {
+      switch (mt) {
+        case 1: go(conv_k3pair_kernel<1, SK, false>); break;
+        case 2: go(conv_k3pair_kernel<2, SK, false>); break;
+        case 3: go(conv_k3pair_kernel<3, SK, false>); break;
+        default: go(conv_k3pair_kernel<4, SK, false>); break;
+      }
     }
-  }
+  };
+  sk ? pick(std::true_type{}) : pick(std::false_type{});
   return hipGetLastError();
 }
 

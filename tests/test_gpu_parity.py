@@ -525,8 +525,8 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
 
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
-                                      {"NIC_K3P": "0"}],
-                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused"])
+                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}],
+                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the
@@ -540,10 +540,10 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
-    if switches in ({"NIC_D8G": "l"}, {"NIC_K3P": "0"}):
+    if switches in ({"NIC_D8G": "l"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}):
         # the LDS-staged gather sums the same projections in the same order as the direct one,
         # and the fused k3 residual pair runs the same MFMA chains and epilogues as the two
-        # weight-stationary launches: bit-identical outputs
+        # weight-stationary launches (in either step order): bit-identical outputs
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from alt_kernels_check import alt_cases
 
