@@ -958,6 +958,22 @@ int grow_pinned(uint8_t*& p, size_t& have, size_t need) {
   return NIC_OK;
 }
 
+// Host-side wait for an event: polling hipEventQuery (default) returns as soon as the GPU
+// signals, where hipEventSynchronize may sleep and pay a wake-up latency per chunk
+// (NIC_HOST_SPIN=0 for the runtime's wait).
+hipError_t host_wait(hipEvent_t e) {
+  static const bool spin = [] {
+    const char* v = getenv("NIC_HOST_SPIN");
+    return !(v && v[0] == '0');
+  }();
+  if (!spin) return hipEventSynchronize(e);
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    __builtin_ia32_pause();
+  }
+}
+
 int host_setup(nic_ctx* c) {
   for (int i = 0; i < 3; ++i) {
     if (!c->hs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking));
@@ -1029,7 +1045,7 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     ++issued;
   }
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
-    hipError_t e = hipEventSynchronize(c->hev[2][k]);
+    hipError_t e = host_wait(c->hev[2][k]);
     if (e != hipSuccess) {
       err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
       break;
