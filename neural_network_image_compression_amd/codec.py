@@ -185,7 +185,7 @@ class Codec:
         n = int(np.prod(shape))
         return torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True).numpy()[:n].reshape(shape)
 
-    def encode_host(self, x: np.ndarray, chunks: int = 4) -> np.ndarray:
+    def encode_host(self, x: np.ndarray, chunks: int = 3) -> np.ndarray:
         """(N,H,W,3) u8 host array -> (N,ceil(H/8),ceil(W/8),96) u8 host array (synchronous)."""
         torch = _torch()
         x = np.ascontiguousarray(x, dtype=np.uint8)
@@ -199,7 +199,7 @@ class Codec:
         _lib.check(rc, "nic_encode_host")
         return z
 
-    def decode_host(self, z: np.ndarray, chunks: int = 4) -> np.ndarray:
+    def decode_host(self, z: np.ndarray, chunks: int = 3) -> np.ndarray:
         """(N,h,w,96) u8 host array -> (N,8h,8w,3) u8 host array (synchronous)."""
         torch = _torch()
         z = np.ascontiguousarray(z, dtype=np.uint8)
@@ -300,8 +300,10 @@ class Codec:
 class ProClass:
     """utils.py:15-62: shared Y/CbCr model holder (kind 'encoder' or 'decoder')."""
 
-    #: chunks of the native host-array pipeline per call (nic_encode_host / nic_decode_host)
-    host_chunks = 4
+    #: chunks of the native host-array pipeline per call (nic_encode_host / nic_decode_host):
+    #: 3 ramped chunks measured fastest for the config-2 batch (2.00 vs 2.07 ms for 4, 2.08 for
+    #: 2; descending / ascending chunk sizes no better, profiles/r3n_host_plan_sweep.txt)
+    host_chunks = 3
 
     kind = ""
 

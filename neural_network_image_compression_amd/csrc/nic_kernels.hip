@@ -2479,7 +2479,6 @@ constexpr int K3P_RW = K3P_MAX_W + 4;               // records per LDS row (66 u
 constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 17,408 B
 constexpr int K3P_NI = 5, K3P_NC = 4;               // input / conv_a ring rows
 constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 156,672 B
-constexpr int K3P_SR = 16;                          // least output rows per block
 
 __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
 
@@ -4182,8 +4181,16 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   a.tiles_x = k3pair_strips(a.W);
   const long long rows = (long long)a.P * a.tiles_x * a.H;
   if (rows == 0) return hipSuccess;
-  // at least K3P_SR rows per block (fill / drain amortised), at most one block per CU
-  const int grid = (int)std::max(1LL, std::min<long long>((rows + K3P_SR - 1) / K3P_SR, device_cus()));
+  // at most one block per CU, at least `sr` rows per block (NIC_K3P_SR, default 4): a block's
+  // fixed cost is 3 pipeline fill steps and 2 recomputed conv_a rows, so small batches (the
+  // host surface's chunks: 11-21 images) are faster spread over every CU with few rows each
+  // than on fewer CUs with more (16 rows per block left 124 of 256 CUs idle at 11 images)
+  static const int sr = [] {
+    const char* e = getenv("NIC_K3P_SR");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 64 ? v : 4;
+  }();
+  const int grid = (int)std::max(1LL, std::min<long long>((rows + sr - 1) / sr, device_cus()));
   const int mt = (a.W + 15) / 16;
   // SKEW (default; NIC_K3P_SK=0 for the lockstep order): conv_b runs each row's epilogue at the
   // start of the next step, beside conv_a's MFMA stream, instead of after its own stream

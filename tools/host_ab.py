@@ -42,6 +42,9 @@ def main():
         return round(float(np.median(ts)) * 1e3, 3)
 
     res = {"device_ms": med(lambda: c.decode(c.encode(xd)))}
+    zd = c.encode(xd)
+    res["dev_enc_4x16_ms"] = med(lambda: [c.encode(xd[k:k + 16]) for k in range(0, 64, 16)])
+    res["dev_dec_4x16_ms"] = med(lambda: [c.decode(zd[k:k + 16]) for k in range(0, 64, 16)])
     z = enc(xh)
     for k in (int(v) for v in args.chunks.split(",")):
         enc.host_chunks = dec.host_chunks = k
