@@ -20,6 +20,8 @@
  *   Training step convolutions, forward and     nic_conv_gather / nic_conv_wgrad /
  *     backward (tf2_0/src/training.py:74-151,     nic_absmax_scale / nic_gauss_1d
  *     Keras Conv2D / Conv2DTranspose SAME, SSIM)  (training side path)
+ *   Training step optimiser (training.py:147-149, nic_adam_keras
+ *     tf.keras Adam)
  *
  * Conventions
  *  - Every buffer argument is a DEVICE pointer owned by the caller (e.g. a torch-ROCm
@@ -211,7 +213,12 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
  *     split-f16 operands keep every bit of tiny gradients; work >= 512 floats.
  * nic_gauss_1d: one-channel planes (n,h,w): VALID correlation with ntaps taps along x
  *     (vertical 0) or y, or its adjoint (the input gradient); the SSIM loss's separable
- *     Gaussian (tf.image.ssim, training.py:119-121). */
+ *     Gaussian (tf.image.ssim, training.py:119-121).
+ * nic_adam_keras: the step's optimiser update (training.py:147-149, tf.keras Adam = TF's
+ *     ResourceApplyAdam) over `count` tensors in one launch; table = device int64 records
+ *     {var, m, v, grad, n} (pointers to fp32 device buffers, n elements), max_n their largest n:
+ *       m += (g - m)*(1 - beta1);  v += (g*g - v)*(1 - beta2);  var -= (m*alpha)/(sqrt(v) + epsilon)
+ *     each op an fp32 rounding; alpha = lr*sqrt(1 - beta2^t)/(1 - beta1^t) from the caller. */
 int nic_conv_gather_work(int kh, int kw, int cin, int cout, int64_t* bytes);
 int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
                     int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
@@ -224,6 +231,8 @@ int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float*
 int nic_absmax_scale(const float* x, int64_t count, float* scale, float* work, void* stream);
 int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, int ntaps, int vertical, int adjoint,
                  float* out, int h_out, int w_out, void* stream);
+int nic_adam_keras(const int64_t* table, int count, int64_t max_n, float alpha, float beta1, float beta2,
+                   float epsilon, void* stream);
 
 /* Per-layer device timing.  With timing on, every kernel launch of encode/decode is
  * bracketed by a hipEvent pair on the caller's stream (the stream the kernel runs on);

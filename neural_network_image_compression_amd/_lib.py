@@ -81,6 +81,7 @@ _SIGNATURES = {
     "nic_absmax_scale": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp, c_vp]),
     "nic_gauss_1d": (ctypes.c_int, [c_vp] + [ctypes.c_int] * 3 + [c_vp] + [ctypes.c_int] * 3 + [c_vp]
                      + [ctypes.c_int] * 2 + [c_vp]),
+    "nic_adam_keras": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int64] + [ctypes.c_float] * 4 + [c_vp]),
 }
 
 

@@ -1277,6 +1277,16 @@ int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, 
   return NIC_OK;
 }
 
+int nic_adam_keras(const int64_t* table, int count, int64_t max_n, float alpha, float beta1, float beta2,
+                   float epsilon, void* stream) {
+  if (count < 0 || count > 65535 || max_n < 0) return fail(NIC_ESHAPE, "nic_adam_keras: bad count %d / max_n %lld", count, (long long)max_n);
+  if (count == 0 || max_n == 0) return NIC_OK;
+  if (!table) return fail(NIC_EINVAL, "nic_adam_keras: NULL table");
+  HIP_TRY(launch_adam_keras((const long long*)table, count, (long long)max_n, alpha, beta1, beta2, epsilon,
+                            (hipStream_t)stream));
+  return NIC_OK;
+}
+
 int nic_absmax_scale(const float* x, int64_t count, float* scale, float* work, void* stream) {
   if (count < 0) return fail(NIC_ESHAPE, "nic_absmax_scale: negative count");
   if (!scale || !work || (count > 0 && !x)) return fail(NIC_EINVAL, "nic_absmax_scale: NULL argument");

@@ -200,6 +200,9 @@ hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, cons
 hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb,
                              int kh, int kw, int stride, int pad_y, int pad_x, const float* gat_scale,
                              const float* dir_scale, float* dw, float* work, hipStream_t st);
+// tf.keras Adam over `count` tensors (table: {var, m, v, grad, n} int64 records on the device)
+hipError_t launch_adam_keras(const long long* table, int count, long long max_n, float alpha, float beta1,
+                             float beta2, float eps, hipStream_t st);
 hipError_t launch_gauss1d(const float* in, int n, int hi, int wi, const float* taps, int nt, int vertical, int adjoint,
                           float* out, int ho, int wo, hipStream_t st);
 

@@ -2449,6 +2449,180 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 }
 
 // ------------------------------------------------------------------------------------
+// dconv1 (Conv2DTranspose 32 -> 64, k5 s2 on the dequantised latent, decoder.py:10,20,40-41)
+// as a persistent weight-stationary kernel on the u8 codes.  The one-tile-per-block form
+// (conv_x3_kernel, NIC_D1=x) re-reads all 25 taps of weights from L2 per block (205 KB x
+// 1,536 blocks) and issues ~9 VALU per MFMA around a latency-bound pipeline (PMC: issue stall
+// 0.60, MFMA busy 0.23).  Here, as in dconv7's all-phase blocks: wave w owns output channels
+// 16w..16w+15 and keeps one sub-pixel phase's taps resident (A operand: w_hi, w_lo of 32
+// input channels per tap = 8 VGPRs), a block walks its share of the model's 8 x 8 coarse
+// tiles once per phase, and the codes (0..255, exact in f16) are the B operand: 2 MFMAs per
+// MAC, 1/255 folded into the epilogue scale (one rounding, as conv_x3_kernel).  Halo: 10 x 10
+// coarse pixels of 32 codes, loaded to registers one tile ahead (during the current tile's
+// MFMA stream) and written to LDS as f16 records of 80 B (5 slots) in rows of 896 B: for
+// every tap the 16 lanes of a B-fragment ds_read_b128 group (two 8-pixel rows) hit 16
+// distinct 4-bank slots (20 r mod 64 for the 8 pixels of a row, + 32 for the second).
+// ------------------------------------------------------------------------------------
+constexpr int D1_PSB = 80;           // LDS bytes per halo pixel: 32 f16 codes + 16 pad
+constexpr int D1_RPB = 896;          // halo row pitch (10 pixels + pad): 224 words = 32 mod 64
+constexpr int D1_HB = 10 * D1_RPB;   // one halo buffer
+constexpr int D1_LD = 4;             // code dwords per thread per tile (800 over 256 threads)
+
+template <int KH, int KW>
+__device__ __forceinline__ void d1_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
+                                        int px) {
+  constexpr int COUT = 64, MT = 4, NTAPS = KH * KW, TAP_BYTES = 32 * COUT * 4, PXB = COUT * 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int per_plane = a.tiles_y * a.tiles_x;
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  const int ntot = np * per_plane;
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  if (ntile == 0) return;
+
+  // resident weights of this phase: A fragment (row co = 16w + l16, k = channel 8g + j) is the
+  // f16x3 repack's 16-B chunk (k16-step g/2, half g%2) -- the ws_body formula with one k32-step
+  f16x8 wr[NTAPS][2];
+  {
+    const char* wsrc = (const char*)a.wx + ((size_t)model * 25 + tb) * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl)
+        wr[t][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
+                                    ((((g >> 1) * 2 + hl) * 2 + (g & 1)) * COUT + wave * 16 + l16) * 16);
+  }
+  // 2^-k undoes the weight pre-scale and carries the dequantiser's 1/255: fma(sum, s, b)
+  const float scale = a.wscale[model] * 0.0039215688593685627f;
+  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + wave * 16 + 4 * g);
+
+  // code staging: thread q = threadIdx.x + 256 j loads dword q & 7 (codes 4c..4c+3) of halo
+  // pixel q >> 3 (row hy, column hx; origin (t0y - 1, t0x - 1))
+  int st_lds[D1_LD], st_hy[D1_LD], st_hx[D1_LD];
+#pragma unroll
+  for (int j = 0; j < D1_LD; ++j) {
+    const int q = threadIdx.x + 256 * j, pix = q >> 3, c = q & 7;
+    st_hy[j] = q < 800 ? pix / 10 : -1000;  // -1000: no dword (out of every image)
+    st_hx[j] = pix - (pix / 10) * 10;
+    st_lds[j] = (pix / 10) * D1_RPB + st_hx[j] * D1_PSB + c * 8;
+  }
+  // codes of the next tile in registers (loads two tiles ahead, 2 x 4 registers, measured
+  // slower: 0.0705 vs 0.0658 ms)
+  uint32_t cq[D1_LD];
+  TileWalk it_ld, it_ep;
+  it_ld.init(bi, nb, a.tiles_y, a.tiles_x);
+  it_ep = it_ld;
+  auto load_codes = [&] {  // the next tile's codes into cq (zeros outside the image)
+    int pl, ty, tx;
+    it_ld.take(pl, ty, tx);
+    const int p = p0 + pl;
+    const uint8_t* base = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
+#pragma unroll
+    for (int j = 0; j < D1_LD; ++j) {
+      const int gy = ty * 8 - 1 + st_hy[j], gx = tx * 8 - 1 + st_hx[j];
+      const bool ok = (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+      cq[j] = ok ? *(const uint32_t*)(base + ((size_t)gy * a.W + gx) * 96 + (threadIdx.x & 7) * 4) : 0u;
+    }
+  };
+  auto write_codes = [&](char* buf) {  // cq -> f16 codes (exact) in LDS
+#pragma unroll
+    for (int j = 0; j < D1_LD; ++j) {
+      if (st_hy[j] < 0) continue;
+      const uint32_t q = cq[j];
+      const f16x4 c = {(_Float16)(float)(q & 255), (_Float16)(float)((q >> 8) & 255),
+                       (_Float16)(float)((q >> 16) & 255), (_Float16)(float)(q >> 24)};
+      *(f16x4*)(buf + st_lds[j]) = c;
+    }
+  };
+
+  // B fragment of pixel tile m (coarse pixels (2m + l16/8, l16%8)) at tap (kh, kw): chunk g
+  int bx[KW];
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw) bx[kw] = (l16 >> 3) * D1_RPB + ((l16 & 7) + kw) * D1_PSB + g * 16;
+  // output granules (fine pixel (2y + py, 2x + px)) through a per-plane buffer resource
+  const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
+  const unsigned out_plane = (unsigned)((size_t)a.OH * a.OW * PXB);
+  unsigned g_off[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int dy = 2 * m + (l16 >> 3), dx = l16 & 7;
+    g_off[m] = (unsigned)(((2 * dy) * a.OW + 2 * dx) * PXB + st_off * 2);
+  }
+  f32x4 acc[MT];
+  float rmax = 0.f;
+  int ep_p = 0, ep_y = 0, ep_x = 0;
+  load_codes();
+  for (int i = 0; i <= ntile; ++i) {
+    char* buf = lds + (i & 1) * D1_HB;
+    if (i < ntile) write_codes(buf);  // buffer i & 1 was last read by tile i-2's stream
+    lds_reads_done();                 // this wave's code writes have landed
+    stage_barrier();                  // tile i's halo complete; tile i-1's stream done everywhere
+    if (i > 0) {  // epilogue of tile i-1: *2^-k/255, bias, leaky, split, 16-B stores
+      const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.out_s + (size_t)ep_p * out_plane / 2), (short)0, (int)out_plane, kBufWord3);
+      const unsigned out_org = (unsigned)(((2 * ep_y + py) * a.OW + 2 * ep_x + px) * PXB);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+        const bool in = y < a.H && x < a.W;
+        if (in) range_track(rmax, v);
+        f16x4 hi, lo;
+        split4(v, hi, lo);
+        const u32x4 q = swap16_pair(hi, lo);
+        __builtin_amdgcn_raw_buffer_store_b128(q, out_rs, in ? out_org + g_off[m] : kDmaOOR, 0, 0);
+      }
+    }
+    if (i == ntile) break;
+    {
+      int pl, ty, tx;
+      it_ep.take(pl, ty, tx);
+      ep_p = p0 + pl;
+      ep_y = ty * 8;
+      ep_x = tx * 8;
+    }
+    if (i + 1 < ntile) load_codes();  // lands during this tile's stream
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const unsigned bb = lds_off(buf);
+    auto frag = [&](int m, int t) {
+      const int kh = t / KW, kw = t - kh * KW;
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(bb + bx[kw]) + (2 * m + kh) * D1_RPB);
+    };
+    f16x8 fb[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) fb[m] = frag(m, 0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][1], fb[m], acc[m], 0, 0, 0);  // w_lo*c
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][0], fb[m], acc[m], 0, 0, 0);  // w_hi*c
+        if (t + 1 < NTAPS) fb[m] = frag(m, t + 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  range_report(a.rg, rmax);
+}
+
+// Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi (Y, CbCr); every block
+// runs the four sub-pixel phases over its share of the model's tiles (as dconv7's blocks)
+__global__ __launch_bounds__(256, 2) void dconv1_ws_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * D1_HB];
+  const int gi = (int)blockIdx.x >= a.ws_blk[1] ? 1 : 0;
+  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  d1_body<3, 3>(a, lds, gi, bi, nb, 16, 1, 1);
+  d1_body<2, 3>(a, lds, gi, bi, nb, 4, 0, 1);
+  d1_body<3, 2>(a, lds, gi, bi, nb, 10, 1, 0);
+  d1_body<2, 2>(a, lds, gi, bi, nb, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------
 // Fused residual pair of the k3 s1 layers: out = leaky(conv_b(leaky(conv_a(x) + b_a)) + b_b) + x
 // (encoder.py:22-25 conv3 -> conv4 -> + res; decoder.py:26-29 dconv5 -> dconv6 -> + res, the
 // Conv2DTranspose k3 s1 layers repacked as flipped convs).  Split-f16 in and out.
@@ -4286,11 +4460,12 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
   return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
 }
 
+static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st);
 static int dconv1_variant() {
   static const int v = [] {
     const char* e = getenv("NIC_D1");
     return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5
-                  : e[0] == '8' ? 6 : 0;
+                  : e[0] == '8' ? 6 : e[0] == 'x' ? 7 : 0;
   }();
   return v;
 }
@@ -4322,10 +4497,11 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
         // NIC_D1=8: the 8x8-tile form on codes (0.0785-0.0789 vs 0.0763-0.0765 ms for the
         // default, same box)
         case 6: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        // default: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
+        // NIC_D1=x: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
         // epilogue; NIC_D1=s the split dequantised activations, 3 MFMAs, round 2) on 8x16
-        // coarse tiles, 4 waves
-        default: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        // coarse tiles, 4 waves, one tile per block (round-3 default before dconv1_ws_kernel)
+        case 7: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        default: return launch_dconv1_ws(a, st);
       }
     case L_DCONV5:
       if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
@@ -4375,6 +4551,31 @@ static char d8_mode() {
 static bool use_d8_strip() { return d8_mode() != 't'; }
 
 bool dconv78_fused() { return use_ws() && d8_mode() == 'p'; }
+
+// dconv1 on the u8 codes, persistent weight-stationary (dconv1_ws_kernel): two block groups
+// (Y, CbCr) in proportion to their planes, two blocks per CU
+static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st) {
+  a.tiles_y = (a.H + 7) / 8;
+  a.tiles_x = (a.W + 7) / 8;
+  const long long per_plane = (long long)a.tiles_y * a.tiles_x, nt = per_plane * a.P;
+  if (nt == 0) return hipSuccess;
+  if (nt > INT32_MAX || a.P != 3 * a.nimg || a.OH != 2 * a.H || a.OW != 2 * a.W || !a.in_u8) return hipErrorInvalidValue;
+  if ((long long)a.OH * a.OW * 256 >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit granule offsets
+  static const int bpc = [] {  // resident blocks per CU (NIC_D1_BPC; 156 VGPRs allow 3)
+    const char* e = getenv("NIC_D1_BPC");
+    const int v = e ? atoi(e) : 2;
+    return v >= 1 && v <= 3 ? v : 2;
+  }();
+  const long long target = (long long)bpc * device_cus();
+  const long long ty = (long long)a.nimg * per_plane, tc = 2LL * a.nimg * per_plane;
+  const int by = (int)std::max(1LL, std::min(ty, (target + 1) / 3)), bc = (int)std::max(1LL, std::min(tc, target - by));
+  a.ws_ngrp = 2;
+  a.ws_blk[0] = 0;
+  a.ws_blk[1] = by;
+  a.ws_blk[2] = by + bc;
+  hipLaunchKernelGGL(dconv1_ws_kernel, dim3(by + bc), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
   if (!a.proj || !a.proj_w || a.OH != 2 * a.H || a.OW != 2 * a.W) return hipErrorInvalidValue;

@@ -657,4 +657,50 @@ hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, co
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// tf.keras Adam (training.py:147-149 `optimizer.apply_gradients`; Keras' OptimizerV2 Adam calls
+// TensorFlow's ResourceApplyAdam with use_nesterov = false) over many tensors in one launch.
+// TF's ApplyAdam functor (training_ops, published algorithm; TF is not in the reference tree):
+//   alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)     (host, fp32, as Keras' iteration powers)
+//   m += (g - m) * (1 - beta1);  v += (g * g - v) * (1 - beta2)
+//   var -= (m * alpha) / (sqrt(v) + epsilon)
+// every op an fp32 rounding in that order (no contraction: -ffp-contract=off; sqrt and the
+// division correctly rounded, as NumPy's fp32 ops: the GPU test is bit-exact against them).  Block (x, k) updates elements [4 * 256 * x, ...) of tensor k,
+// whose {var, m, v, grad, n} record is table[5k .. 5k+4].
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_keras_kernel(const long long* __restrict__ table, float alpha, float b1c,
+                                                         float b2c, float eps) {
+  const long long* r = table + 5 * blockIdx.y;
+  float* var = (float*)r[0];
+  float* m = (float*)r[1];
+  float* v = (float*)r[2];
+  const float* g = (const float*)r[3];
+  const long long n = r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long i = ((long long)blockIdx.x * 4 + k) * 256 + threadIdx.x;
+    if (i >= n) break;
+    const float gi = g[i];
+    const float mi = __fadd_rn(m[i], __fmul_rn(__fsub_rn(gi, m[i]), b1c));
+    const float vi = __fadd_rn(v[i], __fmul_rn(__fsub_rn(__fmul_rn(gi, gi), v[i]), b2c));
+    m[i] = mi;
+    v[i] = vi;
+    // sqrt correctly rounded: the f64 square root rounded to f32 (double rounding is exact for
+    // sqrt at 53 >= 2 x 24 + 2 bits; v_sqrt_f32 alone is within 1 ulp, not correctly rounded)
+    const float sv = (float)__dsqrt_rn((double)vi);
+    var[i] = __fsub_rn(var[i], __fdiv_rn(__fmul_rn(mi, alpha), __fadd_rn(sv, eps)));
+  }
+}
+
+hipError_t launch_adam_keras(const long long* table, int count, long long max_n, float alpha, float beta1,
+                             float beta2, float eps, hipStream_t st) {
+  if (count <= 0 || max_n <= 0) return hipSuccess;
+  const long long bx = (max_n + 1023) / 1024;
+  if (bx > INT32_MAX || count > 65535) return hipErrorInvalidValue;
+  const float b1c = 1.0f - beta1, b2c = 1.0f - beta2;  // fp32, as T(1) - beta
+  hipLaunchKernelGGL(adam_keras_kernel, dim3((unsigned)bx, (unsigned)count), dim3(256), 0, st, table, alpha, b1c, b2c,
+                     eps);
+  return hipGetLastError();
+}
+
 }  // namespace nic

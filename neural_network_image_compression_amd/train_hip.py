@@ -254,3 +254,52 @@ def gauss_valid(t, g1d):
     x = _fns()[2].apply(t.reshape(n, h, w), g1d, 0)
     x = _fns()[2].apply(x, g1d, 1)
     return x.reshape(n, 1, x.shape[1], x.shape[2])
+
+
+def keras_adam_alpha(step: int, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999) -> float:
+    """alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t) in fp32, with Keras' fp32 iteration powers
+    (``local_step = iterations + 1``; ``pow(beta, local_step)``) -- the scalar of TF's ApplyAdam."""
+    import numpy as np
+
+    f = np.float32
+    b1p, b2p = np.power(f(beta1), f(step)), np.power(f(beta2), f(step))
+    return float(f(f(lr) * np.sqrt(f(1) - b2p)) / (f(1) - b1p))
+
+
+class KerasAdam:
+    """tf.keras.optimizers.Adam(lr) (training.py:149) on HIP: one ``nic_adam_keras`` launch per
+    step over every parameter of the model (m and v kept per parameter, zero-initialised like
+    Keras' slots), the update in TF's ApplyAdam order in fp32.  ``step(grads)`` takes the
+    gradients in the order of ``params``."""
+
+    def __init__(self, params, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999, epsilon: float = 1e-7):
+        torch = _torch()
+        self.params = list(params)
+        dev = _same_device(*self.params)
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise TypeError("KerasAdam: parameters must be contiguous float32 tensors")
+        self.lr, self.beta1, self.beta2, self.epsilon = lr, beta1, beta2, epsilon
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.iterations = 0
+        self.device = dev
+        self.max_n = max((p.numel() for p in self.params), default=0)
+
+    def step(self, grads) -> None:
+        torch = _torch()
+        grads = [g.detach().contiguous() for g in grads]
+        if len(grads) != len(self.params):
+            raise ValueError("KerasAdam.step: one gradient per parameter")
+        for p, g in zip(self.params, grads):
+            if g.shape != p.shape or g.dtype != torch.float32 or g.device != p.device:
+                raise ValueError("KerasAdam.step: gradient shape / dtype / device differs from its parameter")
+        self.iterations += 1
+        alpha = keras_adam_alpha(self.iterations, self.lr, self.beta1, self.beta2)
+        rows = [[p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), p.numel()]
+                for p, m, v, g in zip(self.params, self.m, self.v, grads)]
+        with torch.cuda.device(self.device):
+            table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(self.device, non_blocking=True)
+            _lib.check(_lib.lib().nic_adam_keras(table.data_ptr(), len(rows), self.max_n, alpha, self.beta1, self.beta2,
+                                                 self.epsilon, _stream(self.device)), "nic_adam_keras")
+        self._keep = (table, grads)  # alive until the stream has run the launch

@@ -263,8 +263,15 @@ class Training:
         if self.entropy_model is None:
             self.entropy_model = Entropynet((-(-hw[0] // 8), -(-hw[1] // 8)), self.device, self.seed)
         if self._opt is None:
-            # tf.keras.optimizers.Adam(1e-4): beta 0.9 / 0.999, epsilon 1e-7 (see keras_adam_eps)
-            mk = lambda ps: torch.optim.Adam(ps, lr=1e-4, betas=(0.9, 0.999), eps=KERAS_ADAM_EPS)  # noqa: E731
+            # tf.keras.optimizers.Adam(1e-4): beta 0.9 / 0.999, epsilon 1e-7 -- on HIP, TF's
+            # ApplyAdam update in fp32 (train_hip.KerasAdam, one launch per model); on the torch
+            # backend torch.optim.Adam with Keras' epsilon-hat (see keras_adam_eps)
+            if self.hip:
+                from .train_hip import KerasAdam
+
+                mk = lambda ps: KerasAdam(ps, lr=1e-4, beta1=0.9, beta2=ADAM_BETA2, epsilon=KERAS_ADAM_EPS)  # noqa: E731
+            else:
+                mk = lambda ps: torch.optim.Adam(ps, lr=1e-4, betas=(0.9, ADAM_BETA2), eps=KERAS_ADAM_EPS)  # noqa: E731
             self._opt = (mk(self._variables("Y")), mk(self._variables("CbCr")), mk(self.entropy_model.parameters()))
 
     def train_step(self, images, entropy_loss_coef: float, flip: bool = True) -> Dict[str, object]:
@@ -282,6 +289,9 @@ class Training:
         ge = torch.autograd.grad(aprox_entropy_loss, ent_params)
         for opt, params, grads in ((opt_y, self._variables("Y"), gy), (opt_c, self._variables("CbCr"), gc),
                                    (opt_e, ent_params, ge)):
+            if self.hip:
+                opt.step(grads)
+                continue
             for prm, g in zip(params, grads):
                 prm.grad = g
             for group in opt.param_groups:  # Keras' epsilon-hat at this step (keras_adam_eps)

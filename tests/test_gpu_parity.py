@@ -525,8 +525,8 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
 
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
-                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}],
-                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep"])
+                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}, {"NIC_D1": "x"}],
+                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "dconv1-tile"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the

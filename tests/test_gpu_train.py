@@ -167,3 +167,52 @@ def test_strided_operands_and_scale():
     assert torch.equal(y_view, y_copy)
     with pytest.raises(TypeError):  # a host operand never reaches the C-ABI
         train_hip.gather(view.contiguous(), kern.cpu(), 0, 1, (1, 1), 0, (12, 9), 64)
+
+
+def _np_keras_adam(var, m, v, g, step, lr=1e-4, b1=0.9, b2=0.999, eps=1e-7):
+    """TF's ApplyAdam (tf.keras Adam, training.py:149) restated in NumPy fp32, op by op:
+    m += (g - m)(1 - b1); v += (g g - v)(1 - b2); var -= (m alpha) / (sqrt(v) + eps)."""
+    from neural_network_image_compression_amd.train_hip import keras_adam_alpha
+
+    f = np.float32
+    alpha = f(keras_adam_alpha(step, lr, b1, b2))
+    b1c, b2c = f(1) - f(b1), f(1) - f(b2)
+    m = m + (g - m) * b1c
+    v = v + (g * g - v) * b2c
+    var = var - (m * alpha) / (np.sqrt(v) + f(eps))
+    return var, m, v
+
+
+def test_keras_adam_on_hip_matches_tf_formula_bit_exact():
+    # the optimiser step of the HIP training backend (nic_adam_keras, one launch over every
+    # tensor) against the fp32 NumPy restatement of TF's ApplyAdam: bit-identical over 3 steps,
+    # tensor sizes around the 1,024-element block boundary; and within fp32 rounding of
+    # torch.optim.Adam with Keras' epsilon-hat (training.keras_adam_eps)
+    from neural_network_image_compression_amd.train_hip import KerasAdam
+
+    rng = np.random.default_rng(5)
+    sizes = [(5, 5, 32, 64), (64,), (1023,), (1025,), (1,), (3, 3, 64, 64)]
+    host = [rng.standard_normal(s).astype(np.float32) for s in sizes]
+    params = [torch.from_numpy(h.copy()).cuda() for h in host]
+    ref = [torch.from_numpy(h.copy()).cuda().requires_grad_() for h in host]
+    opt = KerasAdam(params)
+    topt = torch.optim.Adam(ref, lr=1e-4, betas=(0.9, 0.999), eps=1e-7)
+    var = [h.copy() for h in host]
+    m = [np.zeros_like(h) for h in host]
+    v = [np.zeros_like(h) for h in host]
+    for step in range(1, 4):
+        grads = [rng.standard_normal(s).astype(np.float32) * np.float32(10.0 ** -step) for s in sizes]
+        opt.step([torch.from_numpy(g).cuda() for g in grads])
+        for i, g in enumerate(grads):
+            var[i], m[i], v[i] = _np_keras_adam(var[i], m[i], v[i], g, step)
+            ref[i].grad = torch.from_numpy(g).cuda()
+        for group in topt.param_groups:
+            group["eps"] = T.keras_adam_eps(step)
+        topt.step()
+        torch.cuda.synchronize()
+        for i in range(len(sizes)):
+            np.testing.assert_array_equal(params[i].cpu().numpy(), var[i], err_msg=f"var {i} step {step}")
+            np.testing.assert_array_equal(opt.m[i].cpu().numpy(), m[i])
+            np.testing.assert_array_equal(opt.v[i].cpu().numpy(), v[i])
+            d = (params[i] - ref[i].detach()).abs().max().item()
+            assert d <= 1e-6 * max(1.0, ref[i].detach().abs().max().item()), (i, step, d)
