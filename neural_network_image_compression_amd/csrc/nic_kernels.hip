@@ -1378,6 +1378,12 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
   auto issue = [&](int i) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
     tile_take(it_issue, p, t0y, t0x);
+#ifdef NIC_DIAG_ONETILE  // diagnostic build only: every tile reads the halo of tile (1,1) of its
+                         // model's first plane (input from L2; wrong results)
+    p = p0;
+    t0y = TH;
+    t0x = TW;
+#endif
     if constexpr (kBufHalo)
       hp.issue(lds + (i & 1) * G::HALO_BYTES, (const char*)a.in_s + (size_t)p * plane_bytes, plane_bytes, a.W,
                t0y - a.pad_y, t0x - a.pad_x, wave);
@@ -1444,6 +1450,9 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     }
   };
   auto proj_dst = [&] {  // a.proj block of the tile whose epilogue just ran (ep_*)
+#ifdef NIC_DIAG_ONEPROJ  // diagnostic build only: every tile writes the same projection block
+    return a.proj + (size_t)(blockIdx.x & 7) * (25 * 64) + 16 * wave + 4 * g;
+#endif
     return a.proj + ((((size_t)ep_p * 4 + 2 * py + px) * a.tiles_y + ep_y / TH) * a.tiles_x + ep_x / TW) * (25 * 64) +
            16 * wave + 4 * g;
   };
