@@ -2468,12 +2468,14 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 // tiles once per phase, and the codes (0..255, exact in f16) are the B operand: 2 MFMAs per
 // MAC, 1/255 folded into the epilogue scale (one rounding, as conv_x3_kernel).  Halo: 10 x 10
 // coarse pixels of 32 codes, loaded to registers one tile ahead (during the current tile's
-// MFMA stream) and written to LDS as f16 records of 80 B (5 slots) in rows of 896 B: for
-// every tap the 16 lanes of a B-fragment ds_read_b128 group (two 8-pixel rows) hit 16
-// distinct 4-bank slots (20 r mod 64 for the 8 pixels of a row, + 32 for the second).
+// MFMA stream) and written to LDS as f16 records of 64 B (4 slots) in rows of 800 B (50 slots):
+// for every tap column, each of ds_read_b128's four lane groups ({0-3,12-15,20-27}, ...; lane
+// (g, l16) reads slot g of pixel (l16 / 8, l16 % 8 + kw)) hits 16 distinct 16-B bank slots
+// (exhaustive search over record / row pitches and chunk swizzles; the first layout, 80-B
+// records in 896-B rows, had 50 % LDS bank-conflict cycles by PMC).
 // ------------------------------------------------------------------------------------
-constexpr int D1_PSB = 80;           // LDS bytes per halo pixel: 32 f16 codes + 16 pad
-constexpr int D1_RPB = 896;          // halo row pitch (10 pixels + pad): 224 words = 32 mod 64
+constexpr int D1_PSB = 64;           // LDS bytes per halo pixel: 32 f16 codes, unpadded
+constexpr int D1_RPB = 800;          // halo row pitch (10 pixels + 160 B): 50 slots = 2 mod 16
 constexpr int D1_HB = 10 * D1_RPB;   // one halo buffer
 constexpr int D1_LD = 4;             // code dwords per thread per tile (800 over 256 threads)
 
