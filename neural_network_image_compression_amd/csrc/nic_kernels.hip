@@ -2663,6 +2663,12 @@ constexpr int K3P_REC = 256;                        // split record: 64 ch x [hi
 constexpr int K3P_RW = K3P_MAX_W + 4;               // records per LDS row (66 used, whole DMA pieces)
 constexpr int K3P_ROWB = K3P_RW * K3P_REC;          // 17,408 B
 constexpr int K3P_NI = 5, K3P_NC = 4;               // input / conv_a ring rows
+// skewed pair: the next input row's DMA issued by conv_b after its deferred epilogue
+// (NIC_K3P_DMAB=1) instead of by conv_a at the step start, whose stream then starts at once
+#ifndef NIC_K3P_DMAB
+#define NIC_K3P_DMAB 1
+#endif
+constexpr bool kK3pDmaB = NIC_K3P_DMAB != 0;
 constexpr int K3P_LDS = (K3P_NI + K3P_NC) * K3P_ROWB;  // 156,672 B
 
 __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_REC + ((chunk ^ ((2 * rec) & 15)) << 4); }
@@ -2739,7 +2745,7 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
     const int npiece = STRIP ? K3P_RW / 4 : (W * 16 + 63) / 64;
     const int xi0 = STRIP ? sx0 - 2 : -1;
     char* dst = in_ring + slot * K3P_ROWB + rec0 * K3P_REC;
-    if (SKEW && role) return;
+    if (SKEW && role == (kK3pDmaB ? 0 : 1)) return;
     for (int k = SKEW ? w : wave; k < npiece; k += SKEW ? 4 : 8) {
       const int q = 64 * k + lane, rec = rec0 + (q >> 4), x = xi0 + rec, ch = (q & 15) ^ ((2 * rec) & 15);
       const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && rec < K3P_MAX_W + 2;
@@ -2872,7 +2878,8 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
 #endif
         // the next input row lands during this step.  (SKEW: issuing conv_a's pieces inside its
         // MFMA stream instead measured no faster -- 4 LDS-DMA issues cost ~700 cycles either way)
-        if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);
+        // kK3pDmaB: conv_b issues it, after its deferred epilogue once it has rows (j >= 3)
+        if (j <= nrow && !(SKEW && kK3pDmaB && ROLE == 1 && j >= 3)) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);
 #ifdef NIC_STAMPS
         NIC_PNOW(s_b);
         s_dma += s_b - s_a;
@@ -2921,6 +2928,9 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
               s_epi += s_e1 - s_e0;
 #endif
             }
+            // slot (j + 3) % 5 held row y4 - 1's residual, in registers since the last step
+            if constexpr (kK3pDmaB)
+              if (j <= nrow) dma_row(rs_in, r0 + j + 1, (j + 3) % K3P_NI);
             conv_row(cb0, cb1, cb2, [](int) {});
             load_res(res);  // row y4's residual, read before the next step's DMA reuses its slot
           } else {
@@ -2937,8 +2947,11 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
         NIC_PNOW(s_a);
 #endif
         if (ROLE == 1 && (SKEW || j >= 3)) {
-          if constexpr (!SKEW) __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
-        } else {
+          if constexpr (!SKEW)
+            __builtin_amdgcn_s_waitcnt(0x0F70 | MT);  // vmcnt(MT), expcnt 7, lgkmcnt 15
+          else if constexpr (kK3pDmaB)
+            dma_wait_all();  // conv_b's pieces of the next row (and its older output stores)
+        } else if (!(SKEW && kK3pDmaB)) {
           dma_wait_all();
         }
         lds_reads_done();  // and its LDS reads / conv_a writes are done
