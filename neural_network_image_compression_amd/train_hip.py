@@ -285,6 +285,17 @@ class KerasAdam:
         self.iterations = 0
         self.device = dev
         self.max_n = max((p.numel() for p in self.params), default=0)
+        # the {var, m, v, grad, n} table: a pinned host copy (only the gradient pointers change
+        # between steps) and its device twin, reused every step
+        import numpy as np
+
+        n = len(self.params)
+        self._host = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
+        self._hnp = self._host.numpy()
+        for i, (p, m, v) in enumerate(zip(self.params, self.m, self.v)):
+            self._hnp[i] = (p.data_ptr(), m.data_ptr(), v.data_ptr(), 0, p.numel())
+        self._dev = torch.empty((n, 5), dtype=torch.int64, device=dev)
+        self._copied = None  # event: the last table upload has read the pinned buffer
 
     def step(self, grads) -> None:
         torch = _torch()
@@ -296,10 +307,14 @@ class KerasAdam:
                 raise ValueError("KerasAdam.step: gradient shape / dtype / device differs from its parameter")
         self.iterations += 1
         alpha = keras_adam_alpha(self.iterations, self.lr, self.beta1, self.beta2)
-        rows = [[p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr(), p.numel()]
-                for p, m, v, g in zip(self.params, self.m, self.v, grads)]
         with torch.cuda.device(self.device):
-            table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(self.device, non_blocking=True)
-            _lib.check(_lib.lib().nic_adam_keras(table.data_ptr(), len(rows), self.max_n, alpha, self.beta1, self.beta2,
-                                                 self.epsilon, _stream(self.device)), "nic_adam_keras")
-        self._keep = (table, grads)  # alive until the stream has run the launch
+            if self._copied is not None:
+                self._copied.synchronize()  # the previous upload has read the pinned table
+            for i, g in enumerate(grads):
+                self._hnp[i, 3] = g.data_ptr()
+            self._dev.copy_(self._host, non_blocking=True)
+            self._copied = torch.cuda.Event()
+            self._copied.record()
+            _lib.check(_lib.lib().nic_adam_keras(self._dev.data_ptr(), len(grads), self.max_n, alpha, self.beta1,
+                                                 self.beta2, self.epsilon, _stream(self.device)), "nic_adam_keras")
+        self._keep = grads  # alive until the stream has run the launch

@@ -234,6 +234,7 @@ class Training:
         if backend not in ("hip", "torch"):
             raise ValueError(f"backend must be 'hip' or 'torch', not {backend!r}")
         self.hip = backend == "hip"
+        self.hip_adam = True  # HIP backend: the Keras Adam update on HIP (False: torch.optim.Adam)
         self.device = torch.device(device)
         w = weights if weights is not None else W.seeded_weights(seed, init="glorot")  # Keras defaults
         self.params = {k: torch.tensor(np.asarray(v, np.float32), device=self.device, requires_grad=True)
@@ -266,7 +267,7 @@ class Training:
             # tf.keras.optimizers.Adam(1e-4): beta 0.9 / 0.999, epsilon 1e-7 -- on HIP, TF's
             # ApplyAdam update in fp32 (train_hip.KerasAdam, one launch per model); on the torch
             # backend torch.optim.Adam with Keras' epsilon-hat (see keras_adam_eps)
-            if self.hip:
+            if self.hip and self.hip_adam:
                 from .train_hip import KerasAdam
 
                 mk = lambda ps: KerasAdam(ps, lr=1e-4, beta1=0.9, beta2=ADAM_BETA2, epsilon=KERAS_ADAM_EPS)  # noqa: E731
@@ -289,7 +290,7 @@ class Training:
         ge = torch.autograd.grad(aprox_entropy_loss, ent_params)
         for opt, params, grads in ((opt_y, self._variables("Y"), gy), (opt_c, self._variables("CbCr"), gc),
                                    (opt_e, ent_params, ge)):
-            if self.hip:
+            if not isinstance(opt, torch.optim.Optimizer):  # train_hip.KerasAdam
                 opt.step(grads)
                 continue
             for prm, g in zip(params, grads):
