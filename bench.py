@@ -255,8 +255,13 @@ def launch_check(world: int, rank: int) -> None:
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group(os.environ.get("NIC_BENCH_BACKEND", "nccl"))
+        # gloo by default: the probe tensor is a host tensor (RCCL would need it on
+        # cuda:LOCAL_RANK); NIC_BENCH_BACKEND=nccl moves it to the rank's GPU
+        backend = os.environ.get("NIC_BENCH_BACKEND", "gloo")
+        dist.init_process_group(backend)
         t = torch.tensor([1.0])
+        if backend == "nccl":
+            t = t.to(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}")
         dist.all_reduce(t)
         ranks = int(t.item())
         dist.destroy_process_group()

@@ -178,11 +178,26 @@ int nic_ms_ssim(nic_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int h, 
  * bytes_per_image bytes: sse (n,) uint64.  PSNR = 10 log10(255^2 * bytes / sse). */
 int nic_sq_err(const uint8_t* a, const uint8_t* b, int n, int64_t bytes_per_image, uint64_t* sse, void* stream);
 
-/* PNG byte count of each of m u8 images (h, w, channels = 1 or 3) in HOST memory, exactly as
- * Pillow writes it with optimize=True (the reference's save_img, utils.py:85-87): adaptive
- * per-row filter (least sum of |signed bytes|), zlib level 9 / window 15 / memLevel 9 /
- * Z_FILTERED, 65,536-B IDATs.  get_bpp (training.py:12-21) is 8 * sizes[i] / pixels.  Host
- * threads only (threads >= 1), no GPU, no ctx.  w * channels <= 16384. */
+/* PNG files of m u8 images (h, w, channels = 1 or 3) in HOST memory, on `threads` host
+ * threads (no GPU, no ctx; w * channels <= 16384), in one of two encoders' settings:
+ *   NIC_PNG_PILLOW  Pillow with optimize=True, the reference's bitstream writer save_img
+ *                   (utils.py:85-87): adaptive per-row filter (least sum of |signed bytes|,
+ *                   first on ties), zlib level 9 / window 15 / memLevel 9 / Z_FILTERED,
+ *                   65,536-B IDATs -- byte for byte Pillow's file (tests/test_png_encode.py;
+ *                   Pillow and this library link the same zlib 1.2.11 here).
+ *   NIC_PNG_TF      tf.image.encode_png(compression=-1), what get_bpp sizes
+ *                   (training.py:12-21): libpng 1.6 defaults -- the same filter heuristic,
+ *                   zlib default level (6) / memLevel 8 / Z_FILTERED, libpng's window
+ *                   reduction and CMF rewrite for small images, 8,192-B IDATs.  TensorFlow is
+ *                   not importable here: parity with its own output is UNPINNED.
+ * nic_png_encode writes file i at out + i * out_stride (out_stride >= nic_png_bound; out may
+ * be NULL for sizes only) and its byte count to sizes[i].  nic_png_sizes = the Pillow sizes
+ * (the val_bpp of training.py:157-163 and the RD harness). */
+#define NIC_PNG_PILLOW 0
+#define NIC_PNG_TF 1
+int nic_png_bound(int h, int w, int channels, int mode, int64_t* bytes);
+int nic_png_encode(const uint8_t* images, int m, int h, int w, int channels, int mode, uint8_t* out,
+                   int64_t out_stride, int64_t* sizes, int threads);
 int nic_png_sizes(const uint8_t* images, int m, int h, int w, int channels, int64_t* sizes, int threads);
 
 /* Bitstream image layout of ProClass._feed_batch: (n,h8,w8,96) <-> (n,4*h8,8*w8,3), each

@@ -63,6 +63,9 @@ _SIGNATURES = {
     "nic_set_range_policy": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_range_trips": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int64)]),
     "nic_png_sizes": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int]),
+    "nic_png_bound": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp]),
+    "nic_png_encode": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp,
+                                      ctypes.c_int64, c_vp, ctypes.c_int]),
     "nic_rerun_launch_info": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_int)]),
     "nic_set_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),

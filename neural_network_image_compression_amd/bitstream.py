@@ -47,33 +47,72 @@ def png_bytes(img: np.ndarray, optimize: bool = True) -> bytes:
     return buf.getvalue()
 
 
-def png_sizes(images: np.ndarray, threads: int = 16) -> np.ndarray:
-    """len(png_bytes(a)) of every u8 image a of images (M, H, W) or (M, H, W, 3), computed
-    natively (nic_png_sizes: Pillow's row filters + zlib level 9 on host threads, no Python
-    per image) -- byte for byte the size Pillow writes."""
+PNG_MODES = {"pillow": 0, "tf": 1}  # nic.h NIC_PNG_PILLOW / NIC_PNG_TF
+
+
+def _png_shape(images: np.ndarray, fn: str):
+    a = np.ascontiguousarray(images, dtype=np.uint8)
+    if a.ndim not in (3, 4) or (a.ndim == 4 and a.shape[3] != 3):
+        raise ValueError(f"{fn}: expected (M, H, W) or (M, H, W, 3) images, got shape {a.shape}")
+    return a, a.shape[0], a.shape[1], a.shape[2], 3 if a.ndim == 4 else 1
+
+
+def png_sizes(images: np.ndarray, threads: int = 16, mode: str = "pillow") -> np.ndarray:
+    """PNG byte counts of every u8 image of images (M, H, W) or (M, H, W, 3), computed natively
+    on host threads (nic_png_encode without output).  mode "pillow": len(png_bytes(a)) byte for
+    byte (save_img, utils.py:85-87); mode "tf": tf.image.encode_png(compression=-1)'s settings,
+    what get_bpp sizes (training.py:12-21; parity with TF itself unpinned, nic.h)."""
     import ctypes
 
     from . import _lib
 
-    a = np.ascontiguousarray(images, dtype=np.uint8)
-    if a.ndim not in (3, 4) or (a.ndim == 4 and a.shape[3] != 3):
-        raise ValueError(f"png_sizes: expected (M, H, W) or (M, H, W, 3) images, got shape {a.shape}")
-    m, h, w = a.shape[:3]
-    ch = 3 if a.ndim == 4 else 1
+    a, m, h, w, ch = _png_shape(images, "png_sizes")
     out = np.empty(m, np.int64)
     if m:
-        _lib.check(_lib.lib().nic_png_sizes(a.ctypes.data_as(ctypes.c_void_p), m, h, w, ch,
-                                            out.ctypes.data_as(ctypes.c_void_p), int(threads)), "nic_png_sizes")
+        _lib.check(_lib.lib().nic_png_encode(a.ctypes.data_as(ctypes.c_void_p), m, h, w, ch, PNG_MODES[mode], None, 0,
+                                             out.ctypes.data_as(ctypes.c_void_p), int(threads)), "nic_png_encode")
     return out
 
 
+def png_encode(images: np.ndarray, threads: int = 16, mode: str = "pillow") -> List[bytes]:
+    """The PNG files of every u8 image of images (M, H, W) or (M, H, W, 3), encoded natively on
+    host threads (nic_png_encode); mode "pillow" is byte for byte Pillow's optimize=True file."""
+    import ctypes
+
+    from . import _lib
+
+    a, m, h, w, ch = _png_shape(images, "png_encode")
+    if m == 0:
+        return []
+    L = _lib.lib()
+    stride = ctypes.c_int64()
+    _lib.check(L.nic_png_bound(h, w, ch, PNG_MODES[mode], ctypes.byref(stride)), "nic_png_bound")
+    buf = np.empty((m, stride.value), np.uint8)
+    sizes = np.empty(m, np.int64)
+    _lib.check(L.nic_png_encode(a.ctypes.data_as(ctypes.c_void_p), m, h, w, ch, PNG_MODES[mode],
+                                buf.ctypes.data_as(ctypes.c_void_p), stride.value,
+                                sizes.ctypes.data_as(ctypes.c_void_p), int(threads)), "nic_png_encode")
+    return [buf[i, :sizes[i]].tobytes() for i in range(m)]
+
+
 def save_img(img: np.ndarray, output_dir: str, filename: str) -> str:
-    """utils.py:85-87."""
-    assert (np.round(img) - img).sum() == 0
-    path = os.path.join(output_dir, filename + ".png")
-    with open(path, "wb") as f:
-        f.write(png_bytes(np.asarray(img, dtype=np.uint8)))
-    return path
+    """utils.py:85-87 (the file Pillow's optimize=True writes, encoded natively)."""
+    return save_imgs(np.asarray(img)[None], output_dir, [filename], threads=1)[0]
+
+
+def save_imgs(imgs: np.ndarray, output_dir: str, filenames: Sequence[str], threads: int = 16) -> List[str]:
+    """save_img (utils.py:85-87) of a batch of equal-shaped images: the PNG files encoded on
+    ``threads`` native host threads (nic_png_encode, byte-identical to Pillow), then written."""
+    imgs = np.asarray(imgs)
+    assert (np.round(imgs) - imgs).sum() == 0  # utils.py:86
+    files = png_encode(imgs.astype(np.uint8), threads=threads)
+    paths = []
+    for data, name in zip(files, filenames):
+        path = os.path.join(output_dir, name + ".png")
+        with open(path, "wb") as f:
+            f.write(data)
+        paths.append(path)
+    return paths
 
 
 def png_bpp(packed: np.ndarray, pixels: int, optimize: bool = True) -> float:
@@ -93,12 +132,12 @@ def _batches(shapes: Sequence[tuple], batch_size: int):
 
 
 def feed_batch(model, x: np.ndarray, filenames: Sequence[str], output_dir: str, in_cshape: int,
-               pool=None) -> list:
+               pool=None, png_threads: int = 16) -> list:
     """utils.py:30-44 for one batch: unpack (decoder side), run the codec, pack (encoder side), save.
 
-    With a thread pool the PNG writes (zlib, which runs without the GIL inside Pillow) are
-    submitted to it and their futures returned, so the caller can run the next batch on the
-    GPU while this one is being compressed on the host cores."""
+    The batch's PNG files are encoded natively on ``png_threads`` host threads (nic_png_encode,
+    byte-identical to Pillow's optimize=True).  With a pool the encode + write is submitted to
+    it and its future returned, so the caller runs the next batch on the GPU meanwhile."""
     import torch
 
     codec = model.codec
@@ -110,11 +149,16 @@ def feed_batch(model, x: np.ndarray, filenames: Sequence[str], output_dir: str, 
     if out.shape[-1] == 96:
         out = codec.pack(out)
     host = out.cpu().numpy()
-    if pool is None:
+    if host.shape[1] == 1 or host.shape[2] == 1:  # np.squeeze (utils.py:44) changes the mode
         for i in range(host.shape[0]):
-            save_img(np.squeeze(host[i]), output_dir, filenames[i])
+            a = np.squeeze(host[i])
+            save_imgs(a[None], output_dir, [filenames[i]], threads=1)
         return []
-    return [pool.submit(save_img, np.squeeze(host[i]), output_dir, filenames[i]) for i in range(host.shape[0])]
+    imgs = host
+    if pool is None:
+        save_imgs(imgs, output_dir, filenames, threads=png_threads)
+        return []
+    return [pool.submit(save_imgs, imgs, output_dir, list(filenames), png_threads)]
 
 
 def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, in_cshape: int,

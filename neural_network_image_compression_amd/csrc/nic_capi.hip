@@ -506,7 +506,7 @@ int nic_create(int device, nic_ctx** out) {
     return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
   }
   if (hipMalloc(&c->range, 8 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(int)) != hipSuccess ||
-      hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&c->range_host, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: range-guard allocation failed");
   }
@@ -891,6 +891,17 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
 // run the exact-fp32 kernels (64-bit addressing) instead of failing (nic.h).
 bool x3_plane_fits(long long h64, long long w64) { return h64 * w64 * 64 * 4 < (1LL << 30); }
 
+// The chained re-run's barrier timeout (nic_kernels.hip grid_barrier), read from words[4] of
+// c->range with the device idle: reported once as NIC_EHIP, and the barrier words (arrivals,
+// generation, flag) are zeroed so the next chain starts clean (an abandoned barrier leaves
+// bar[0] mid-count; until this clears the sticky flag, every chain on the ctx exits at entry).
+int chain_timeout_check(nic_ctx* c, const int* words, const char* what) {
+  if (!words[4]) return NIC_OK;
+  HIP_TRY(hipMemset(c->range + 2, 0, 3 * sizeof(int)));
+  return fail(NIC_EHIP, "%s: a chained exact-fp32 re-run timed out at its grid barrier (blocks not co-resident); "
+              "the outputs of that pass are undefined", what);
+}
+
 template <class Pass>
 int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pass) {
   if (c->precision != NIC_PRECISION_F16X3 || !x3_fits) return pass(false, RangeGuard{}, true);
@@ -907,8 +918,13 @@ int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pas
     gate.epoch = c->epoch;
     return pass(false, gate, false);
   }
-  HIP_TRY(hipMemcpyAsync(c->range_host, c->range, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (c->range_host[4]) {  // an earlier FALLBACK pass's chain timed out
+    HIP_TRY(hipDeviceSynchronize());
+    rc = chain_timeout_check(c, c->range_host, what);
+    if (rc) return rc;
+  }
   if (*c->range_host == c->epoch) {
     ++c->error_trips;
     return fail(NIC_ERANGE, "%s: an activation reached the f16 limit of the split-f16 pass (|x| >= 65504); "
@@ -1044,6 +1060,12 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     }
     ++issued;
   }
+  // the range-guard words behind the last pass (its chained re-run's barrier timeout flag),
+  // read once the streams drain: this call synchronises anyway
+  const bool chain_check = !err && issued > 0 && c->precision == NIC_PRECISION_F16X3 &&
+                           c->range_policy == NIC_RANGE_FALLBACK;
+  if (chain_check && hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess)
+    err = fail(NIC_EHIP, "host surface: range-word read-back failed");
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
     hipError_t e = host_wait(c->hev[2][k]);
     if (e != hipSuccess) {
@@ -1053,6 +1075,10 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     if (!out_pin) std::memcpy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
   }
   for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);  // drained on every path
+  if (!err && chain_check && c->range_host[4]) {
+    HIP_TRY(hipDeviceSynchronize());
+    err = chain_timeout_check(c, c->range_host, "host surface");
+  }
   return err;
 }
 
@@ -1323,10 +1349,7 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   int words[5] = {};
   HIP_TRY(hipMemcpy(words, c->range, sizeof(words), hipMemcpyDeviceToHost));
   *passes = (int64_t)words[1] + c->error_trips;
-  if (words[4])  // fp32_chain_kernel's grid barrier gave up (nic_kernels.hip grid_barrier)
-    return fail(NIC_EHIP, "nic_range_trips: a chained exact-fp32 re-run timed out at its grid barrier "
-                "(blocks not co-resident); its outputs are undefined");
-  return NIC_OK;
+  return chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
 }
 
 int nic_rerun_launch_info(nic_ctx* c, int* blocks_per_cu, int* grid, int* cooperative) {

@@ -115,6 +115,11 @@ struct Fp32Chain {
   RangeGuard gate;  // gate + trips of the re-run (the stages' own rg fields are unused)
   int* bar;         // 3 zeroed device words: barrier arrivals, generation, timeout flag
   int nstage;
+  // bounded barrier wait (s_memrealtime ticks, 100 MHz; launch_fp32_chain fills it) and a
+  // diagnostic that keeps the grid's last block from ever arriving (NIC_DIAG_BARRIER=skip:
+  // the timeout path's GPU test, tests/barrier_timeout_check.py)
+  unsigned long long timeout_ticks;
+  int diag_skip;
   int kind[kChainMax];      // LayerId; L_CONV1 -> c1, L_DCONV8 -> d8, other layers -> c[s]
   ConvArgs c[kChainMax];
   Conv1Args c1;

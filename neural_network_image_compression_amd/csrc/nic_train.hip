@@ -665,8 +665,8 @@ hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, co
 //   m += (g - m) * (1 - beta1);  v += (g * g - v) * (1 - beta2)
 //   var -= (m * alpha) / (sqrt(v) + epsilon)
 // every op an fp32 rounding in that order (no contraction: -ffp-contract=off; sqrt and the
-// division correctly rounded, as NumPy's fp32 ops: the GPU test is bit-exact against them).  Block (x, k) updates elements [4 * 256 * x, ...) of tensor k,
-// whose {var, m, v, grad, n} record is table[5k .. 5k+4].
+// division correctly rounded, as NumPy's fp32 ops: the GPU test is bit-exact against them).  Block (x, k) updates elements [1024 x, 1024 x + 1024) of
+// tensor k, then the same range one grid-width further on (n > max_n is covered), k's {var, m, v, grad, n} record is table[5k .. 5k+4].
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adam_keras_kernel(const long long* __restrict__ table, float alpha, float b1c,
                                                          float b2c, float eps) {
@@ -676,9 +676,12 @@ __global__ __launch_bounds__(256) void adam_keras_kernel(const long long* __rest
   float* v = (float*)r[2];
   const float* g = (const float*)r[3];
   const long long n = r[4];
+  // grid-stride over the record: a record longer than the max_n that sized the grid is
+  // still updated whole
+  for (long long base = (long long)blockIdx.x * 1024; base < n; base += (long long)gridDim.x * 1024)
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const long long i = ((long long)blockIdx.x * 4 + k) * 256 + threadIdx.x;
+    const long long i = base + k * 256 + threadIdx.x;
     if (i >= n) break;
     const float gi = g[i];
     const float mi = __fadd_rn(m[i], __fmul_rn(__fsub_rn(gi, m[i]), b1c));

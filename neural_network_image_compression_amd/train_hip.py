@@ -292,10 +292,27 @@ class KerasAdam:
         n = len(self.params)
         self._host = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
         self._hnp = self._host.numpy()
-        for i, (p, m, v) in enumerate(zip(self.params, self.m, self.v)):
-            self._hnp[i] = (p.data_ptr(), m.data_ptr(), v.data_ptr(), 0, p.numel())
+        self._fill_table()
         self._dev = torch.empty((n, 5), dtype=torch.int64, device=dev)
         self._copied = None  # event: the last table upload has read the pinned buffer
+
+    def _fill_table(self) -> None:
+        for i, (p, m, v) in enumerate(zip(self.params, self.m, self.v)):
+            self._hnp[i] = (p.data_ptr(), m.data_ptr(), v.data_ptr(), 0, p.numel())
+        self._ptrs = [p.data_ptr() for p in self.params]
+
+    def _check_table(self) -> None:
+        """A parameter rebound since the table was built (p.data = ..., a reload into new
+        tensors) would leave the kernel writing through a stale pointer: re-point the table
+        at the current storage (same shapes: the m / v slots still fit)."""
+        torch = _torch()
+        if all(p.data_ptr() == q for p, q in zip(self.params, self._ptrs)):
+            return
+        for p, m in zip(self.params, self.m):
+            if p.shape != m.shape or p.dtype != torch.float32 or not p.is_contiguous() or p.device != m.device:
+                raise TypeError("KerasAdam: a parameter was rebound to a tensor of another shape / dtype / "
+                                "layout / device")
+        self._fill_table()
 
     def step(self, grads) -> None:
         torch = _torch()
@@ -310,6 +327,7 @@ class KerasAdam:
         with torch.cuda.device(self.device):
             if self._copied is not None:
                 self._copied.synchronize()  # the previous upload has read the pinned table
+            self._check_table()
             for i, g in enumerate(grads):
                 self._hnp[i, 3] = g.data_ptr()
             self._dev.copy_(self._host, non_blocking=True)

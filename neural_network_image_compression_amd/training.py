@@ -150,14 +150,16 @@ def ssim(x, y, max_val: float = 1.0, hip: bool = False):
     return (lum * cs).mean(dim=(1, 2, 3))
 
 
-def png_bpp_planes(encoded_u8: np.ndarray, tot_pixels: float, threads: int = 16) -> np.ndarray:
+def png_bpp_planes(encoded_u8: np.ndarray, tot_pixels: float, threads: int = 16, mode: str = "tf") -> np.ndarray:
     """get_bpp (training.py:14-21): latent planes (M,h,w,32) u8 -> (M,) 8*len(PNG((4h,8w)))/pixels.
 
-    The PNG sizes are Pillow's own byte counts (save_img's encoder, utils.py:85-87), computed
-    natively on ``threads`` host threads (bitstream.png_sizes / nic_png_sizes, tested equal to
-    Pillow byte for byte)."""
+    The PNG sizes are computed natively on ``threads`` host threads (bitstream.png_sizes /
+    nic_png_encode).  mode "tf" (default): the settings of ``tf.image.encode_png`` that
+    get_bpp calls (training.py:12: libpng defaults, zlib level 6; parity with TF itself
+    unpinned, nic.h NIC_PNG_TF); mode "pillow": the bytes save_img writes (utils.py:85-87,
+    optimize=True; tested equal to Pillow byte for byte) -- the validation bpp."""
     m, h, w, _ = encoded_u8.shape
-    sizes = png_sizes(encoded_u8.reshape(m, 4 * h, 8 * w), threads)
+    sizes = png_sizes(encoded_u8.reshape(m, 4 * h, 8 * w), threads, mode=mode)
     return (8.0 * sizes.astype(np.float64) / tot_pixels).astype(np.float32)
 
 
@@ -217,10 +219,11 @@ class Training:
     """training.py:44-172.
 
     Parity notes (unpinned: no TF here): the optimiser follows Keras' Adam exactly
-    (:func:`keras_adam_eps`); the entropy net's bpp target uses Pillow's PNG encoder
-    (``png_bpp_planes``, the one the reference's own ``save_img`` uses, utils.py:85-87)
-    where the reference's ``get_bpp`` calls ``tf.image.encode_png`` (training.py:12), so
-    the target's byte counts may differ from TF's by the two zlib front ends."""
+    (:func:`keras_adam_eps`); the entropy net's bpp target sizes the latent planes with
+    ``tf.image.encode_png``'s settings as get_bpp does (training.py:12-21: libpng defaults,
+    zlib level 6, 8 KiB IDATs; ``png_mode`` "tf", nic.h NIC_PNG_TF) -- a restatement of libpng /
+    zlib, not TF's own bytes; validation's val_bpp sizes the files save_img writes (Pillow,
+    optimize=True, byte-identical)."""
 
     def __init__(self, device: str = "cuda", weights: Optional[W.Weights] = None, seed: int = 0,
                  checkpoint_dir: str = "../checkpoints/", backend: Optional[str] = None,
@@ -246,9 +249,10 @@ class Training:
         self._opt = None
         self._gen = torch.Generator(device=self.device).manual_seed(seed)
         # the PNG-size target (get_bpp, training.py:14-21: 3B PNG encodes per step) runs on
-        # host threads (nic_png_sizes) while the device runs the codec's backward: train_step
+        # host threads (nic_png_encode) while the device runs the codec's backward: train_step
         # needs it only for the entropy net's own loss, after the codec gradients are queued
         self.png_threads = png_threads
+        self.png_mode = "tf"  # get_bpp's encoder (training.py:12); "pillow": save_img's
         self._pool = ThreadPoolExecutor(max_workers=1)
 
     def _model(self, name: str) -> Dict[str, object]:
@@ -309,9 +313,9 @@ class Training:
 
     def _png_target(self, codes, pixels: float):
         """Start get_bpp of the step's u8 codes (M,h,w,32) on a host thread: an async copy to
-        page-locked memory, then nic_png_sizes once it has landed.  Returns a future."""
+        page-locked memory, then the native PNG sizes once it has landed.  Returns a future."""
         torch = _torch()
-        threads = self.png_threads
+        threads, mode = self.png_threads, self.png_mode
         if codes.is_cuda:
             host = torch.empty(codes.shape, dtype=torch.uint8, pin_memory=True)
             host.copy_(codes, non_blocking=True)
@@ -320,12 +324,12 @@ class Training:
 
             def job():
                 ev.synchronize()
-                return png_bpp_planes(host.numpy(), pixels, threads)
+                return png_bpp_planes(host.numpy(), pixels, threads, mode)
         else:
             arr = codes.numpy().copy()
 
             def job():
-                return png_bpp_planes(arr, pixels, threads)
+                return png_bpp_planes(arr, pixels, threads, mode)
         return self._pool.submit(job)
 
     def finish_entropy_loss(self, f: Dict[str, object]):

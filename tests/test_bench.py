@@ -21,6 +21,8 @@ def _bench(args, env_extra=None, timeout=300):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     env.update(env_extra or {})
+    for k in [k for k, v in env.items() if v == ""]:
+        env.pop(k)  # "" in env_extra: unset
     return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                           timeout=timeout, cwd=ROOT, env=env)
 
@@ -28,7 +30,8 @@ def _bench(args, env_extra=None, timeout=300):
 def test_bench_gpus_flag_spawns_ranks():
     # `python bench.py --gpus 2` with no launcher starts 2 ranks (torch.distributed.run as a
     # child process); --launch-check stops after the process group (gloo, no GPU work)
-    out = _bench(["--gpus", "2", "--launch-check"], timeout=240)
+    # (NIC_BENCH_BACKEND unset: the launch check's process group defaults to gloo)
+    out = _bench(["--gpus", "2", "--launch-check"], env_extra={"NIC_BENCH_BACKEND": ""}, timeout=240)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]

@@ -412,6 +412,20 @@ def test_f16_range_guard_rerun_variants(switches):
     assert out.returncode == 0 and "RANGE-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
 
 
+def test_chain_barrier_timeout_reported():
+    """The chained re-run's bounded grid barrier: a block that never arrives (diagnostic
+    NIC_DIAG_BARRIER=skip, ~1 ms wait) makes the pass report NIC_EHIP once -- through
+    nic_range_trips, the ERROR policy's synchronising check and the host-array surface --
+    after which the barrier words are clean and the ctx keeps working; child process."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, NIC_DIAG_BARRIER="skip")
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "barrier_timeout_check.py")
+    out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "TIMEOUT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+
+
 def range_guard_contract(golden, weights_spread):
     from neural_network_image_compression_amd import _lib
     from neural_network_image_compression_amd.codec import Codec, Decoder, Encoder

@@ -216,3 +216,42 @@ def test_keras_adam_on_hip_matches_tf_formula_bit_exact():
             np.testing.assert_array_equal(opt.v[i].cpu().numpy(), v[i])
             d = (params[i] - ref[i].detach()).abs().max().item()
             assert d <= 1e-6 * max(1.0, ref[i].detach().abs().max().item()), (i, step, d)
+
+
+def test_keras_adam_rebound_param_and_long_record():
+    # (1) a parameter rebound after construction (p.data = new storage) is followed
+    # -- the update lands in the new tensor, the old one is untouched; (2) a table record longer
+    # than the max_n that sized the grid is still updated whole (the kernel strides over n)
+    import ctypes
+
+    from neural_network_image_compression_amd import _lib
+    from neural_network_image_compression_amd.train_hip import KerasAdam
+
+    rng = np.random.default_rng(9)
+    h = rng.standard_normal(3000).astype(np.float32)
+    p = torch.from_numpy(h.copy()).cuda()
+    opt = KerasAdam([p])
+    old = p.data
+    p.data = torch.from_numpy(h.copy() + 1).cuda()  # rebound: new storage, same shape
+    g = rng.standard_normal(3000).astype(np.float32)
+    opt.step([torch.from_numpy(g).cuda()])
+    torch.cuda.synchronize()
+    var, _, _ = _np_keras_adam(h + np.float32(1), np.zeros_like(h), np.zeros_like(h), g, 1)
+    np.testing.assert_array_equal(p.cpu().numpy(), var)
+    np.testing.assert_array_equal(old.cpu().numpy(), h)
+    # raw C-ABI: one record of n = 5000 launched with max_n = 1000 (grid of one block column)
+    n = 5000
+    v0 = rng.standard_normal(n).astype(np.float32)
+    gv = rng.standard_normal(n).astype(np.float32)
+    var_t, m_t, v_t = torch.from_numpy(v0.copy()).cuda(), torch.zeros(n).cuda(), torch.zeros(n).cuda()
+    g_t = torch.from_numpy(gv).cuda()
+    tab = torch.tensor([[var_t.data_ptr(), m_t.data_ptr(), v_t.data_ptr(), g_t.data_ptr(), n]],
+                       dtype=torch.int64).cuda()
+    from neural_network_image_compression_amd.train_hip import keras_adam_alpha
+    alpha = keras_adam_alpha(1, 1e-4, 0.9, 0.999)
+    L = _lib.lib()
+    _lib.check(L.nic_adam_keras(tab.data_ptr(), 1, 1000, ctypes.c_float(alpha), ctypes.c_float(0.9),
+                                ctypes.c_float(0.999), ctypes.c_float(1e-7), None), "nic_adam_keras")
+    torch.cuda.synchronize()
+    ref, _, _ = _np_keras_adam(v0, np.zeros(n, np.float32), np.zeros(n, np.float32), gv, 1)
+    np.testing.assert_array_equal(var_t.cpu().numpy(), ref)

@@ -37,11 +37,11 @@ def test_png_sizes_multi_idat_and_threads():
 
 
 def test_png_sizes_training_target():
-    # the training step's target: 3B latent planes (B, 16, 16, 32) -> (4*16, 8*16) images
+    # the planes of the training step's target in Pillow's settings (val_bpp's encoder): 3B latent planes (B, 16, 16, 32) -> (4*16, 8*16) images
     from neural_network_image_compression_amd.training import png_bpp_planes
     rng = np.random.default_rng(5)
     z = _planes(rng, 12, 16, 16 * 32, "latent").reshape(12, 16, 16, 32)
-    native = png_bpp_planes(z, 128.0 * 128.0)
+    native = png_bpp_planes(z, 128.0 * 128.0, mode="pillow")  # the TF-settings default: test_png_encode.py
     pillow = np.array([8.0 * len(png_bytes(a)) / (128.0 * 128.0) for a in z.reshape(12, 64, 128)], np.float32)
     np.testing.assert_array_equal(native, pillow)
 

@@ -47,7 +47,7 @@ def main():
     from neural_network_image_compression_amd import weights as W
 
     if not args.png:
-        T.png_bpp_planes = lambda enc, tot, threads=None: np.zeros(enc.shape[0], np.float32)  # device work only
+        T.png_bpp_planes = lambda enc, tot, threads=None, mode=None: np.zeros(enc.shape[0], np.float32)  # device work only
     g = torch.Generator().manual_seed(0)
     imgs = torch.randint(0, 256, (args.batch, args.size, args.size, 3), generator=g, dtype=torch.uint8).cuda()
     w0 = W.seeded_weights(0, init="glorot")
