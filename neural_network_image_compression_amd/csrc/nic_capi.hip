@@ -236,6 +236,32 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
   return repack_x3(outx, 25, cin, cout, get);
 }
 
+// Winograd F(2,3)-along-y kernels of a k3 s1 layer (the fused pair's default form,
+// nic_kernels.hip conv_k3wino_kernel): taps t = 3 xi + kx of
+//   U0 = g0, U1 = ((g0 + g1) + g2) / 2, U2 = ((g0 - g1) + g2) / 2, U3 = g2   (g_ky = kernel row ky)
+// in fp32 from the layer's conv-form kernel (Conv2DTranspose k3 s1: flipped taps, swapped
+// channels, as repack_kernel), then split like any split-f16 kernel.  Returns k of 2^k.
+int repack_wino(const LayerSpec& L, const float* K, std::vector<uint16_t>& outx) {
+  const int k = 3, cin = L.cin, cout = L.cout;
+  auto conv = [&](int t, int ci, int co) {
+    if (!L.transposed) return K[((size_t)t * cin + ci) * cout + co];
+    const int ky = k - 1 - t / k, kx = k - 1 - t % k;
+    return K[(((size_t)ky * k + kx) * cout + co) * cin + ci];
+  };
+  auto get = [&](int t, int ci, int co) {
+    const int xi = t / 3, kx = t % 3;
+    const float g0 = conv(kx, ci, co), g1 = conv(3 + kx, ci, co), g2 = conv(6 + kx, ci, co);
+    switch (xi) {
+      case 0: return g0;
+      case 1: return ((g0 + g1) + g2) * 0.5f;
+      case 2: return ((g0 - g1) + g2) * 0.5f;
+      default: return g2;
+    }
+  };
+  return repack_x3(outx, 12, cin, cout, get);
+}
+bool has_wino(int id) { return id == L_CONV3 || id == L_CONV4 || id == L_DCONV5 || id == L_DCONV6; }
+
 struct SamePad {
   int out, lo;
 };
@@ -267,6 +293,8 @@ struct nic_ctx {
   float* wb[L_COUNT] = {};  // [2 models][cout]
   uint16_t* wx[L_COUNT] = {};  // split-f16 kernels [2 models][taps*cin*cout*2]
   float wscale[L_COUNT][2] = {};  // 2^-k per model for the split-f16 kernels
+  uint16_t* wxw[L_COUNT] = {};    // k3 s1 layers: Winograd U kernels [2 models][12*cin*cout*2] (repack_wino)
+  float wscalew[L_COUNT][2] = {};
   // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
   uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
@@ -499,6 +527,15 @@ int nic_create(int device, nic_ctx** out) {
       (void)hipMemset(c->wb[L.id], 0, bb);
       (void)hipMemset(c->wx[L.id], 0, xb);
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
+      if (has_wino(L.id)) {
+        const size_t wb = 2 * 12 * (size_t)L.cin * L.cout * 2 * sizeof(uint16_t);
+        if (hipMalloc(&c->wxw[L.id], wb) != hipSuccess) {
+          nic_destroy(c);
+          return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
+        }
+        (void)hipMemset(c->wxw[L.id], 0, wb);
+        c->wscalew[L.id][0] = c->wscalew[L.id][1] = 1.0f;
+      }
     }
   }
   if (hipMalloc(&c->wproj, 2 * kProjFrag * 2) != hipSuccess || hipMemset(c->wproj, 0, 2 * kProjFrag * 2) != hipSuccess) {
@@ -538,6 +575,7 @@ int nic_destroy(nic_ctx* c) {
     if (c->wk[i]) (void)hipFree(c->wk[i]);
     if (c->wb[i]) (void)hipFree(c->wb[i]);
     if (c->wx[i]) (void)hipFree(c->wx[i]);
+    if (c->wxw[i]) (void)hipFree(c->wxw[i]);
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
@@ -588,6 +626,13 @@ int nic_set_weights(nic_ctx* c, int model_id, const char* layer, const float* ho
       HIP_TRY(hipMemcpy(c->wx[L->id] + m * packedx.size(), packedx.data(), packedx.size() * sizeof(uint16_t),
                         hipMemcpyHostToDevice));
       c->wscale[L->id][m] = std::ldexp(1.0f, -kexp);
+    }
+    if (has_wino(L->id)) {
+      std::vector<uint16_t> wino;
+      const int kw = repack_wino(*L, host, wino);
+      HIP_TRY(hipMemcpy(c->wxw[L->id] + m * wino.size(), wino.data(), wino.size() * sizeof(uint16_t),
+                        hipMemcpyHostToDevice));
+      c->wscalew[L->id][m] = std::ldexp(1.0f, -kw);
     }
     if (L->id == L_DCONV8) {
       const std::vector<uint16_t> f = proj_fragments(packed, kexp);
@@ -653,6 +698,31 @@ bool use_k3pair() {
     return !(e && e[0] == '0') && conv12_fused();  // conv12_fused(): the weight-stationary set (NIC_WS)
   }();
   return on;
+}
+// NIC_K3P=d: the direct (9-tap) fused pair even where the Winograd pair applies (A/B)
+bool use_k3wino() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_K3P");
+    return use_k3pair() && !(e && e[0] == 'd');
+  }();
+  return on;
+}
+// the fused k3 residual pair of one encoder / decoder pass: Winograd when it takes the plane
+hipError_t launch_pair(nic_ctx* c, ConvArgs ap, LayerId la, LayerId lb, int h, int w, hipStream_t st) {
+  ap.wx2 = c->wx[lb];
+  ap.wscale2[0] = c->wscale[lb][0];
+  ap.wscale2[1] = c->wscale[lb][1];
+  ap.bias2 = c->wb[lb];
+  if (use_k3wino() && k3wino_supported(h, w)) {
+    ap.wxw = c->wxw[la];
+    ap.wscalew[0] = c->wscalew[la][0];
+    ap.wscalew[1] = c->wscalew[la][1];
+    ap.wxw2 = c->wxw[lb];
+    ap.wscalew2[0] = c->wscalew[lb][0];
+    ap.wscalew2[1] = c->wscalew[lb][1];
+    return launch_k3wino_x3(ap, st);
+  }
+  return launch_k3pair_x3(ap, st);
 }
 
 // NIC_CHAIN=0: the gated re-run as one launch per layer (A/B)
@@ -758,12 +828,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {
     // conv3 -> conv4 -> + res as one launch (R1 -> R3, the residual read from the input
     // rows in LDS); timed as conv4
-    ConvArgs ap = conv(L_CONV3, R[1], R[3], nullptr, h2, w2, h2, w2, 1, 1);
-    ap.wx2 = c->wx[L_CONV4];
-    ap.wscale2[0] = c->wscale[L_CONV4][0];
-    ap.wscale2[1] = c->wscale[L_CONV4][1];
-    ap.bias2 = c->wb[L_CONV4];
-    TIMED(L_CONV4, launch_k3pair_x3(ap, st));
+    TIMED(L_CONV4, launch_pair(c, conv(L_CONV3, R[1], R[3], nullptr, h2, w2, h2, w2, 1, 1), L_CONV3, L_CONV4, h2, w2, st));
   } else {
     TIMED(L_CONV3, run(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1)));
     TIMED(L_CONV4, run(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1)));
@@ -832,12 +897,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   TIMED(L_DCONV1, run(L_DCONV1, d1));
   const int h2 = 2 * h8, w2 = 2 * w8;
   if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {  // dconv5 -> dconv6 -> + res, timed as dconv6
-    ConvArgs ap = conv(L_DCONV5, R[1], R[3], nullptr, h2, w2, h2, w2);
-    ap.wx2 = c->wx[L_DCONV6];
-    ap.wscale2[0] = c->wscale[L_DCONV6][0];
-    ap.wscale2[1] = c->wscale[L_DCONV6][1];
-    ap.bias2 = c->wb[L_DCONV6];
-    TIMED(L_DCONV6, launch_k3pair_x3(ap, st));
+    TIMED(L_DCONV6, launch_pair(c, conv(L_DCONV5, R[1], R[3], nullptr, h2, w2, h2, w2), L_DCONV5, L_DCONV6, h2, w2, st));
   } else {
     TIMED(L_DCONV5, run(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2)));
     TIMED(L_DCONV6, run(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2)));

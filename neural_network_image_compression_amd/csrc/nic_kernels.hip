@@ -2998,6 +2998,391 @@ bool k3pair_supported(int H, int W) {
 }
 
 // ------------------------------------------------------------------------------------
+// Fused k3 residual pair on Winograd F(2,3) along y (round 4; the default for planes up to
+// 64 columns; NIC_K3P=d keeps the direct pair above).  conv3 -> conv4 -> + x and
+// dconv5 -> dconv6 -> + x (encoder.py:22-25, decoder.py:26-29) with every conv computed two
+// output rows at a time:
+//   rows d0..d3 = in[y-1 .. y+2] of a pair (y, y+1):  V0 = d0 - d2, V1 = d1 + d2,
+//   V2 = d2 - d1, V3 = d1 - d3;  M_xi[x] = sum_kx sum_ci V_xi[x + kx - 1][ci] U_xi[kx][ci][co]
+//   with U0 = g0, U1 = ((g0 + g1) + g2) / 2, U2 = ((g0 - g1) + g2) / 2, U3 = g2 (g_ky the
+//   kernel row ky);  out[y] = (M0 + M1) + M2,  out[y + 1] = (M1 - M2) - M3.
+// 4 x 3 x 2 k32-steps x 3 split MFMAs per 16 pixels of a pair instead of 2 x 9 x 2 x 3: the
+// split-f16x3 products drop by 1.5x (the pair kernel sits at the chip's power limit, where
+// fewer multiplies, not fewer cycles, are the lever: DESIGN section 5).  The transformed
+// operands are split to f16 hi / lo like any activation (V within 2x of the activations) and
+// the U kernels are pre-scaled per model like the direct kernels (nic_capi.hip repack_wino).
+//
+// Block = 8 waves, one per CU, all 64 columns of a plane, a contiguous range of its row
+// pairs.  Waves 0-3 (A, conv_a, 16 output channels each) and 4-7 (B, conv_b) are SIMD
+// partners; each holds its layer's 12 U fragments x 2 k32-steps x hi / lo (192 VGPRs).  LDS:
+// VI = the four V rows of conv_a's current pair, VB = the four V rows of conv_b's, and one raw
+// input row of staging.  The steps alternate (one barrier each):
+//   A-step i: A runs pair P_i = (r0 + 2i - 1, r0 + 2i) of conv_a from VI and its epilogue
+//             builds conv_b's V rows of pair Q_{i-1} = (r0 + 2i - 2, r0 + 2i - 1) into VB;
+//             B DMAs input row r0 + 2i + 3 into the staging.
+//   B-step i: B runs Q_{i-1} from VB (+ residual, split stores to HBM); A rebuilds VI in
+//             place for P_{i+1} (input rows r0 + 2i .. r0 + 2i + 3).
+// One wave per SIMD issues MFMAs in each step while its partner does the other step's
+// vector work.  The two previous rows a V build needs are not kept anywhere: they are
+// recovered from the V rows being replaced -- d1 + d2 and d2 - d1 give d2 = (V1 + V2) / 2 and
+// d1 = (V1 - V2) / 2, then d3 = d1 - V3 -- exact up to the split rounding (~2^-22 of the
+// activations, not accumulated: each recovered row is formed afresh from a new V row).  The
+// first pair of a segment starts from a VB written to recover (a(r0 - 1), a(r0)) and a VI
+// built from four input rows.
+// Rows outside the plane are zeros (SAME padding); V records of columns -1 and >= 16 MT are
+// zero pads; columns W .. 16 MT - 1 carry zeros from the producers.
+// ------------------------------------------------------------------------------------
+constexpr int K3W_ROWB = K3P_ROWB;                  // one V row: records x = -1 .. 66 (17,408 B)
+constexpr int K3W_SETB = 4 * K3W_ROWB;              // four V rows (69,632 B)
+constexpr int K3W_STGB = 64 * K3P_REC;              // one raw input row (16,384 B)
+constexpr int K3W_LDS = 2 * K3W_SETB + K3W_STGB;    // 155,648 B
+
+// a value the compiler must treat as redefined here: keeps loop-invariant addresses (lane
+// constants) from being hoisted out of the step loop and held in VGPRs across it
+template <class T>
+__device__ __forceinline__ T opaque(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ f32x4 unsplit4(const f16x4& hi, const f16x4& lo) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 H = __builtin_bit_cast(u32x2, hi), L = __builtin_bit_cast(u32x2, lo);
+  return (f32x4){add_f16_pair<0>(H[0], L[0]), add_f16_pair<1>(H[0], L[0]), add_f16_pair<0>(H[1], L[1]),
+                 add_f16_pair<1>(H[1], L[1])};
+}
+// 8 channels: hi chunk h, lo chunk l (16 B each) -> fp32 of channels 2p, 2p + 1
+__device__ __forceinline__ void unsplit_pair(const u32x4& h, const u32x4& l, int p, float& v0, float& v1) {
+  v0 = add_f16_pair<0>(h[p], l[p]);
+  v1 = add_f16_pair<1>(h[p], l[p]);
+}
+// split of two fp32 values into the dword pair (hi, lo) of packed f16 (split4's per-pair body)
+__device__ __forceinline__ void split2(float v0, float v1, unsigned& h, unsigned& l) {
+  float d0, d1;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(v0), "v"(v1));
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(h), "v"(v0));
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(h), "v"(v1));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(d0), "v"(d1));
+}
+
+template <int MT>
+__global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
+  constexpr int COUT = 64, KST = 2;
+  __shared__ __attribute__((aligned(16))) char lds[K3W_LDS];
+  char* vi = lds;
+  char* vb = lds + K3W_SETB;
+  char* stg = lds + 2 * K3W_SETB;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // output channels 16 w ..
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int H = a.H, W = a.W;
+  const int hp = (H + 1) >> 1;  // row pairs per plane
+  const long long total = (long long)a.P * hp;
+  const long long per_block = (total + gridDim.x - 1) / gridDim.x;
+  const long long g0 = (long long)blockIdx.x * per_block, g1 = min(g0 + per_block, total);
+  const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
+
+  // zero pads of both V sets: record 0 (x = -1) and records 16 MT + 1 .. (never written)
+  for (int q = threadIdx.x; q < 8 * (K3W_ROWB / 16); q += 256) {
+    const int row = q / (K3W_ROWB / 16), rq = q - row * (K3W_ROWB / 16), rec = rq >> 4;
+    if (rec == 0 || rec > 16 * MT) *(u32x4*)(lds + row * K3W_ROWB + rq * 16) = (u32x4){0u, 0u, 0u, 0u};
+  }
+
+  // B fragments: pixel 16 m + l16 at tap column kx -> record 16 m + l16 + kx of a V row; lane
+  // group g reads chunk 8 hl + 4 ks + g (the XOR with (2 hl + ks) << 6 selects hl, ks)
+  const unsigned bx0 = (unsigned)k3p_off(l16, g);  // + 256 kx: the swizzle of record l16 + kx
+  const int chunk_st = (g & 1) * 8 + 2 * w + (g >> 1);  // this lane's 16-B granule after swap16_pair
+
+  f16x8 wa[12][KST][2], wb[12][KST][2];  // conv_a / conv_b U fragments of channels 16 w ..
+  int model = -1;
+  float scale_a = 0.f, scale_b = 0.f;
+  f32x4 bias_a = {}, bias_b = {};
+  float rmax = 0.f;
+  auto load_weights = [&](int m) {
+    constexpr int TAP_BYTES = 64 * COUT * 4;
+    const char* sa = (const char*)a.wxw + (size_t)m * 12 * TAP_BYTES;
+    const char* sb = (const char*)a.wxw2 + (size_t)m * 12 * TAP_BYTES;
+#pragma unroll
+    for (int t = 0; t < 12; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          const size_t o = (size_t)t * TAP_BYTES + ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + w * 16 + l16) * 16;
+          wa[t][ks][hl] = *(const f16x8*)(sa + o);
+          wb[t][ks][hl] = *(const f16x8*)(sb + o);
+        }
+    scale_a = a.wscalew[m];
+    scale_b = a.wscalew2[m];
+    bias_a = *(const f32x4*)(a.bias + m * COUT + 16 * w + 4 * g);
+    bias_b = *(const f32x4*)(a.bias2 + m * COUT + 16 * w + 4 * g);
+  };
+
+  // M_xi of pixel tile m over a V set with the U fragments wr (xi-major, 24 steps of 3
+  // MFMAs; B fragments read two steps ahead)
+  f32x4 acc[4];
+  auto mfma_tile = [&](const char* set, const f16x8 (&wr)[12][KST][2], int m) {
+    __builtin_amdgcn_sched_barrier(0);  // the previous tile's epilogue stays ahead of these reads
+    const unsigned b0 = opaque(lds_off(set) + bx0);
+    auto frag = [&](int st, int hl) {
+      const int xi = st / (3 * KST), r = st - xi * 3 * KST, kx = r / KST, ks = r - kx * KST;
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at((b0 + 256u * kx) ^ (unsigned)((2 * hl + ks) << 6)) +
+                                                               xi * K3W_ROWB + m * 16 * K3P_REC);
+    };
+    constexpr int NSTEP = 12 * KST, DEPTH = 2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f16x8 fb[DEPTH][2];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      fb[d][0] = frag(d, 0);
+      fb[d][1] = frag(d, 1);
+    }
+    static_for<NSTEP>([&](auto stc) {
+      constexpr int st = decltype(stc)::value, xi = st / (3 * KST), t = st / KST, ks = st % KST;
+      f16x8(&cur)[2] = fb[st % DEPTH];
+      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], acc[xi], 0, 0, 0);  // u_lo*v_hi
+      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], acc[xi], 0, 0, 0);  // u_hi*v_lo
+      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], acc[xi], 0, 0, 0);  // u_hi*v_hi
+      if constexpr (st + DEPTH < NSTEP) {
+        cur[0] = frag(st + DEPTH, 0);
+        cur[1] = frag(st + DEPTH, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+    });
+  };
+  // the pair's two output rows (fp32, before bias) of the tile just computed
+  auto out_transform = [&](f32x4& y0, f32x4& y1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      y0[r] = __fadd_rn(__fadd_rn(acc[0][r], acc[1][r]), acc[2][r]);
+      y1[r] = __fsub_rn(__fsub_rn(acc[1][r], acc[2][r]), acc[3][r]);
+    }
+  };
+  // this lane's granule (chunk_st) of V row xi, record rec, in VB: read as fp32 (hi + lo of
+  // its 4 channels) / write split
+  auto vrec = [&](int xi, int rec) { return vb + xi * K3W_ROWB + opaque(k3p_off(rec, chunk_st)); };
+  auto read_v = [&](int xi, int rec) {
+    const u32x4 q = *(const u32x4*)vrec(xi, rec);
+    f16x4 hi, lo;
+    unswap16(q, hi, lo);
+    return unsplit4(hi, lo);
+  };
+  auto write_v = [&](int xi, int rec, const f32x4& v) {
+    range_track(rmax, v);
+    f16x4 hi, lo;
+    split4(v, hi, lo);
+    *(u32x4*)vrec(xi, rec) = swap16_pair(hi, lo);
+  };
+
+  // A: conv_a pair (t0, t0 + 1) from VI, then VB for conv_b's pair (t0 - 1, t0) -- or, first
+  // pair of a segment, a VB from which the next build recovers (a(t0), a(t0 + 1))
+  auto a_step = [&](int t0, bool first) {
+    static_for<MT>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      mfma_tile(vi, wa, m);
+      f32x4 y0, y1;
+      out_transform(y0, y1);
+      const int x = 16 * m + l16, rec = x + 1;
+      const bool vx = x < W;
+      const bool v0 = vx && (unsigned)t0 < (unsigned)H, v1 = vx && (unsigned)(t0 + 1) < (unsigned)H;
+      f32x4 a0, a1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a0[r] = v0 ? leaky02(scale_bias(y0[r], scale_a, bias_a[r])) : 0.f;
+        a1[r] = v1 ? leaky02(scale_bias(y1[r], scale_a, bias_a[r])) : 0.f;
+      }
+      if (first) {  // recovers as (p0, p1) = (a0, a1): V1 = V2 = a0, V3 = -a1 (V0 unused)
+        write_v(1, rec, a0);
+        write_v(2, rec, a0);
+        write_v(3, rec, -a1);
+      } else {
+        const f32x4 o1 = read_v(1, rec), o2 = read_v(2, rec), o3 = read_v(3, rec);
+        f32x4 p0, p1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p0[r] = __fmul_rn(__fadd_rn(o1[r], o2[r]), 0.5f);                       // a(t0 - 2)
+          p1[r] = __fsub_rn(__fmul_rn(__fsub_rn(o1[r], o2[r]), 0.5f), o3[r]);     // a(t0 - 1)
+        }
+        f32x4 n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(p0[r], a0[r]);
+        write_v(0, rec, n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) n[r] = __fadd_rn(p1[r], a0[r]);
+        write_v(1, rec, n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(a0[r], p1[r]);
+        write_v(2, rec, n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(p1[r], a1[r]);
+        write_v(3, rec, n);
+      }
+    });
+  };
+
+  // VI for conv_a's pair with input rows d0 = y0 .. d3 = y0 + 3: lane (g, l16) of wave w takes
+  // pixel 16 w + l16 (w < MT) and channel chunks g, 4 + g (B-fragment order: conflict-free
+  // reads), each in two halves of 4 channels; d2 from the prefetch registers, d3 from the
+  // staging row, d0 / d1 recovered from the VI being replaced -- or, first pair of a segment
+  // (FIRST), all four rows from HBM
+  u32x4 pf[2][2];  // the d2 prefetch: [item ks][hi, lo]
+  auto load_item = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int ks, u32x4 (&q)[2]) {
+    const int x = 16 * w + l16;
+    const bool ok = w < MT && (unsigned)y < (unsigned)H && x < W;
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const unsigned off = ok ? (unsigned)((y * W + x) * K3P_REC + (8 * hl + 4 * ks + g) * 16) : kDmaOOR;
+      q[hl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  auto build_vi = [&](const __amdgpu_buffer_rsrc_t& rs, int y0, auto first_c) {
+    constexpr bool FIRST = decltype(first_c)::value;
+    if (w >= MT) return;  // wave-uniform
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int x = 16 * w + l16, rec = x + 1;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 4 * ks + g;
+      u32x4 q0[2], q1[2], q3[2];
+      if constexpr (FIRST) {  // a segment's prologue: latency exposed once per segment
+        load_item(rs, y0, ks, q0);
+        load_item(rs, y0 + 1, ks, q1);
+        load_item(rs, y0 + 2, ks, pf[ks]);
+        load_item(rs, y0 + 3, ks, q3);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        auto at = [&](const char* base, int r, int hl) { return base + opaque(k3p_off(r, 8 * hl + c)) + 8 * h; };
+        auto unsplit2x2 = [&](u32x2 hi, u32x2 lo, float (&o)[4]) {
+          o[0] = add_f16_pair<0>(hi[0], lo[0]);
+          o[1] = add_f16_pair<1>(hi[0], lo[0]);
+          o[2] = add_f16_pair<0>(hi[1], lo[1]);
+          o[3] = add_f16_pair<1>(hi[1], lo[1]);
+        };
+        auto half_of = [&](const u32x4& q) { return (u32x2){q[2 * h], q[2 * h + 1]}; };
+        float d0[4], d1[4], d2[4], d3[4];
+        unsplit2x2(half_of(pf[ks][0]), half_of(pf[ks][1]), d2);
+        if constexpr (FIRST) {
+          unsplit2x2(half_of(q0[0]), half_of(q0[1]), d0);
+          unsplit2x2(half_of(q1[0]), half_of(q1[1]), d1);
+          unsplit2x2(half_of(q3[0]), half_of(q3[1]), d3);
+        } else {
+          unsplit2x2(*(const u32x2*)at(stg, x, 0), *(const u32x2*)at(stg, x, 1), d3);  // staging record = x
+          float v1[4], v2[4], v3[4];
+          unsplit2x2(*(const u32x2*)at(vi + K3W_ROWB, rec, 0), *(const u32x2*)at(vi + K3W_ROWB, rec, 1), v1);
+          unsplit2x2(*(const u32x2*)at(vi + 2 * K3W_ROWB, rec, 0), *(const u32x2*)at(vi + 2 * K3W_ROWB, rec, 1), v2);
+          unsplit2x2(*(const u32x2*)at(vi + 3 * K3W_ROWB, rec, 0), *(const u32x2*)at(vi + 3 * K3W_ROWB, rec, 1), v3);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            d0[e] = __fmul_rn(__fadd_rn(v1[e], v2[e]), 0.5f);                    // d2 of the old pair
+            d1[e] = __fsub_rn(__fmul_rn(__fsub_rn(v1[e], v2[e]), 0.5f), v3[e]);  // its d3
+          }
+        }
+#pragma unroll
+        for (int xi = 0; xi < 4; ++xi) {
+          f32x4 n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            n[e] = xi == 0 ? __fsub_rn(d0[e], d2[e]) : xi == 1 ? __fadd_rn(d1[e], d2[e])
+                 : xi == 2 ? __fsub_rn(d2[e], d1[e]) : __fsub_rn(d1[e], d3[e]);
+          range_track(rmax, n);
+          f16x4 hi, lo;
+          split4(n, hi, lo);
+          *(f16x4*)at(vi + xi * K3W_ROWB, rec, 0) = hi;
+          *(f16x4*)at(vi + xi * K3W_ROWB, rec, 1) = lo;
+        }
+      }
+    }
+  };
+
+  // the staging DMA of input row y (records 0 .. 63, chunk k of record r in slot k ^ (2r & 15))
+  auto dma_stage = [&](const __amdgpu_buffer_rsrc_t& rs, int y) {
+#pragma unroll
+    for (int k = w; k < 16; k += 4) {  // 16 pieces of 1 KB
+      const int q = 64 * k + lane, rec = q >> 4, ch = (q & 15) ^ ((2 * rec) & 15);
+      const bool ok = (unsigned)y < (unsigned)H && rec < W;
+      dma16_buf(rs, ok ? (unsigned)((y * W + rec) * K3P_REC + ch * 16) : kDmaOOR, stg + k * 1024);
+    }
+  };
+  // B: conv_b pair (y, y + 1) from VB, + residual (input rows y, y + 1), split stores
+  auto b_step = [&](const __amdgpu_buffer_rsrc_t& rs_in, const __amdgpu_buffer_rsrc_t& rs_out, int y) {
+    static_for<MT>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      const int x = 16 * m + l16;
+      const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
+      const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
+      const unsigned o1 = o0 + (unsigned)(W * K3P_REC);
+      const u32x4 r0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v0 ? o0 : kDmaOOR, 0, 0));
+      const u32x4 r1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v1 ? o1 : kDmaOOR, 0, 0));
+      mfma_tile(vb, wb, m);
+      f32x4 y0, y1;
+      out_transform(y0, y1);
+      f16x4 rh, rl;
+      unswap16(r0, rh, rl);
+      const f32x4 x0 = unsplit4(rh, rl);
+      unswap16(r1, rh, rl);
+      const f32x4 x1 = unsplit4(rh, rl);
+      f32x4 q0, q1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // x = x + res (encoder.py:25, decoder.py:29)
+        q0[r] = __fadd_rn(leaky02(scale_bias(y0[r], scale_b, bias_b[r])), x0[r]);
+        q1[r] = __fadd_rn(leaky02(scale_bias(y1[r], scale_b, bias_b[r])), x1[r]);
+      }
+      if (v0) range_track(rmax, q0);
+      if (v1) range_track(rmax, q1);
+      f16x4 hi, lo;
+      split4(q0, hi, lo);
+      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out, v0 ? o0 : kDmaOOR, 0, 0);
+      split4(q1, hi, lo);
+      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out, v1 ? o1 : kDmaOOR, 0, 0);
+    });
+  };
+
+  for (long long gs = g0; gs < g1;) {
+    const int p = (int)(gs / hp);
+    const int j0 = (int)(gs - (long long)p * hp), j1 = (int)min((long long)hp, g1 - (long long)p * hp);
+    const int K = j1 - j0, r0 = 2 * j0;
+    gs = (long long)p * hp + j1;
+    const int m_item = p >= a.nimg ? 1 : 0;
+    if (m_item != model) {  // block-uniform: items of one model are consecutive
+      model = m_item;
+      load_weights(model);
+    }
+    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
+    // prologue: VI of P_0 (input rows r0 - 2 .. r0 + 1); the previous segment's last conv_b
+    // pair has read VB and its stores are in flight
+    build_vi(rs_in, r0 - 2, std::true_type{});
+    lds_reads_done();
+    stage_barrier();
+    for (int i = 0; i <= K; ++i) {
+      // A: conv_a pair P_i from VI -> VB (Q_{i-1}); the staging DMA and the d2 prefetch of the
+      // next VI build are issued first so they land during the MFMAs
+      if (i < K) {
+        dma_stage(rs_in, r0 + 2 * i + 3);
+        load_item(rs_in, r0 + 2 * i + 2, 0, pf[0]);
+        load_item(rs_in, r0 + 2 * i + 2, 1, pf[1]);
+      }
+      a_step(r0 + 2 * i - 1, i == 0);
+      dma_wait_all();  // this wave's staging pieces (other waves' lanes read them) and prefetch
+      lds_reads_done();
+      stage_barrier();  // VB of Q_{i-1} and the staging row complete; every wave's VI reads done
+      // B: conv_b pair Q_{i-1} from VB, then the VI of P_{i+1} (in place)
+      if (i >= 1) b_step(rs_in, rs_out, r0 + 2 * i - 2);
+      if (i < K) build_vi(rs_in, r0 + 2 * i, std::false_type{});
+      lds_reads_done();
+      stage_barrier();  // VI of P_{i+1} complete; every wave's VB reads done
+    }
+  }
+  range_report(a.rg, rmax);
+}
+
+bool k3wino_supported(int H, int W) {
+  return H > 0 && W > 0 && W <= K3P_MAX_W && (long long)H * W * K3P_REC < (1LL << 31);
+}
+
+// ------------------------------------------------------------------------------------
 // conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
 // utils.py:74-77).  Block: 16x16 output pixels of one plane, 4 waves x 2 M tiles x 32 co.
 // K = 25 taps padded to 26 (13 MFMAs); lane half h supplies tap 2s+h of step s.
@@ -4396,6 +4781,26 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
 
 // The fused k3 residual pair: persistent blocks (one per CU), each a contiguous range of the
 // planes' rows (planes in order, so a block reloads its weights only when the model changes).
+hipError_t launch_k3wino_x3(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  if (!k3wino_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wxw || !a.wxw2 || !a.bias2 ||
+      a.P != 3 * a.nimg)
+    return hipErrorInvalidValue;
+  const long long pairs = (long long)a.P * ((a.H + 1) / 2);
+  if (pairs == 0) return hipSuccess;
+  // one block per CU, at least 2 row pairs per block (a block's fixed cost: the prologue VI
+  // build from four HBM rows and one recomputed conv_a row)
+  const int grid = (int)std::max(1LL, std::min<long long>((pairs + 1) / 2, device_cus()));
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a); };
+  switch ((a.W + 15) / 16) {
+    case 1: go(conv_k3wino_kernel<1>); break;
+    case 2: go(conv_k3wino_kernel<2>); break;
+    case 3: go(conv_k3wino_kernel<3>); break;
+    default: go(conv_k3wino_kernel<4>); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (!k3pair_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wx2 || !a.bias2 || a.P != 3 * a.nimg)

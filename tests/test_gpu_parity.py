@@ -13,6 +13,7 @@ Parity against TensorFlow itself is unpinned (no TF, no reference fixtures): the
 stands in for it, see oracle/nic_oracle.py.
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -522,10 +523,14 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     assert packed.shape == (64, 128, 3)
     z = codecs["spread"].encode(_dev(g["x"][1:2])).cpu().numpy()
     np.testing.assert_array_equal(packed, O.pack_latent(z)[0])
+    # the file itself is Pillow's optimize=True PNG, byte for byte (native writer, nic_png_encode)
+    from neural_network_image_compression_amd.bitstream import png_bytes
+    assert (tmp_path / "kodak_compressed" / "img1.png").read_bytes() == png_bytes(O.pack_latent(z)[0])
     dec = Decoder(0, precision=codecs["spread"].precision)
     dec.uncompress(str(tmp_path / "kodak_compressed"), str(tmp_path / "ckpt" / "decoder"))
     rec = np.array(Image.open(tmp_path / "kodak_uncompressed" / "img1.png"))
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
+    assert (tmp_path / "kodak_uncompressed" / "img1.png").read_bytes() == png_bytes(rec)
     # threaded PNG writes (workers > 0) produce byte-identical files
     ds2 = tmp_path / "thr"
     ds2.mkdir()
@@ -538,26 +543,33 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
             assert (tmp_path / a / f"img{i}.png").read_bytes() == (tmp_path / b / f"img{i}.png").read_bytes()
 
 
-@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
-                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}, {"NIC_D1": "x"}],
-                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "dconv1-tile"])
-def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
-    """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
-    NIC_D8=tile), and the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip) meet the
-    golden contract too; they run in a child process because the switches are read when
-    the library loads."""
+def _alt_child(tmp_path, switches, tag):
     import os
     import subprocess
     import sys
-    dump = str(tmp_path / "alt.npz")
+    dump = str(tmp_path / f"alt_{tag}.npz")
     env = dict(os.environ, NIC_ALT_DUMP=dump, **switches)
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt_kernels_check.py")
     out = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "ALT-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
-    if switches in ({"NIC_D8G": "l"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}):
-        # the LDS-staged gather sums the same projections in the same order as the direct one,
-        # and the fused k3 residual pair runs the same MFMA chains and epilogues as the two
-        # weight-stationary launches (in either step order): bit-identical outputs
+    return dump
+
+
+@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
+                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0", "NIC_K3P": "d"}, {"NIC_K3P": "d"},
+                                      {"NIC_D1": "x"}],
+                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "k3-direct",
+                              "dconv1-tile"])
+def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
+    """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
+    NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the direct
+    (9-tap) fused k3 pair (NIC_K3P=d), the k3 layers as two launches (NIC_K3P=0) ... meet the
+    golden contract too; they run in a child process because the switches are read when
+    the library loads."""
+    dump = _alt_child(tmp_path, switches, "v")
+    if switches == {"NIC_D8G": "l"}:
+        # the LDS-staged gather sums the same projections in the same order as the direct one:
+        # bit-identical to the default
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from alt_kernels_check import alt_cases
 
@@ -568,3 +580,43 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
         with np.load(dump) as other:
             for k, v in mine.items():
                 np.testing.assert_array_equal(v.cpu().numpy(), other[k], err_msg=k)
+    if switches in ({"NIC_K3P": "0"}, {"NIC_K3P_SK": "0", "NIC_K3P": "d"}):
+        # the direct fused k3 residual pair runs the same MFMA chains and epilogues as the two
+        # weight-stationary launches (in either step order): bit-identical to NIC_K3P=d (the
+        # default Winograd pair is held to the oracle contract instead: test_k3_wino_*)
+        ref = _alt_child(tmp_path, {"NIC_K3P": "d"}, "d")
+        with np.load(dump) as a, np.load(ref) as b:
+            for k in b.files:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_k3_wino_against_direct_pair(tmp_path, weights_spread):
+    """The default k3 pair (Winograd F(2,3) along y, planes up to 64 columns) against the
+    direct 9-tap pair (NIC_K3P=d, child process) on the alt_kernels_check cases: codes and
+    reconstructions within the oracle contract of each other, pre-quant latents within
+    PREQUANT_ATOL (both are within it of the float64 oracle); the max differences are printed."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from alt_kernels_check import alt_cases
+
+    from neural_network_image_compression_amd.codec import Codec
+    ref = _alt_child(tmp_path, {"NIC_K3P": "d"}, "d")
+    c = Codec(0, precision="f16x3")
+    c.set_weights(weights_spread)
+    mine = {k: v.cpu().numpy() for k, v in alt_cases(c).items()}
+    worst = {}
+    with np.load(ref) as b:
+        for k in b.files:
+            if k.endswith("_f") or k.endswith("_z"):
+                continue
+            d = np.abs(mine[k].astype(int) - b[k].astype(int)).max()
+            assert d <= 1, (k, d)
+            worst[k] = int(d)
+        for k in b.files:
+            if k.endswith("_f"):
+                d = float(np.abs(mine[k] - b[k]).max())
+                assert d <= PREQUANT_ATOL, (k, d)
+                worst[k] = d
+                z = k[:-2] + "_z"
+                flips = np.abs(mine[z].astype(int) - b[z].astype(int))
+                assert flips.max() <= 1 and flips.mean() <= 1e-3, (z, flips.max(), flips.mean())
+    print("wino vs direct:", worst)

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=0, help="stop each run after this many steps (0: all epochs)")
     ap.add_argument("--coefs", default="0.01,0.02,0.03")
+    ap.add_argument("--seeds", default="0", help="weight-init / shuffling seeds per coefficient (label suffix _sN for N > 0)")
+    ap.add_argument("--png-mode", default="tf", choices=("tf", "pillow"),
+                    help="the PNG encoder of the entropy net's target (get_bpp: tf.image.encode_png settings)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     x = load_patches(args.data)
@@ -55,10 +58,12 @@ def main():
     with np.load(os.path.join(ROOT, "tests", "golden", "kodim21_full.npz"), allow_pickle=False) as g:
         ev = g["x"]  # the reference's data/kodak_img/kodim21.png, (1, 512, 768, 3)
     sets, train_log = {}, {}
-    for coef in (float(c) for c in args.coefs.split(",")):
+    runs = [(float(c), int(sd)) for c in args.coefs.split(",") for sd in args.seeds.split(",")]
+    for coef, seed in runs:
         t0 = time.perf_counter()
         with tempfile.TemporaryDirectory() as d:
-            tr = T.Training(device="cuda", weights=W.seeded_weights(0, init="glorot"), seed=0, checkpoint_dir=d + "/")
+            tr = T.Training(device="cuda", weights=W.seeded_weights(seed, init="glorot"), seed=seed, checkpoint_dir=d + "/")
+            tr.png_mode = args.png_mode
             epochs = args.epochs
             if args.steps:
                 epochs = min(epochs, -(-args.steps * args.batch // args.epoch_samples))
@@ -71,14 +76,14 @@ def main():
             tr._save()
             w = W.load(os.path.join(d, "encoder"), "encoder")
             w.update(W.load(os.path.join(d, "decoder"), "decoder"))
-        label = f"coef{coef:.2f}"
+        label = f"coef{coef:.2f}" + (f"_s{seed}" if seed else "")
         sets[label] = w
         if args.save_dir:
             os.makedirs(args.save_dir, exist_ok=True)
             for kind in ("encoder", "decoder"):  # <dir>/<label>_encoderY.safetensors, ...
                 W.save(w, os.path.join(args.save_dir, f"{label}_{kind}"), kind)
         tail = log[-20:]
-        train_log[label] = {"steps": len(log), "epochs": epochs, "seconds": round(time.perf_counter() - t0, 1),
+        train_log[label] = {"steps": len(log), "epochs": epochs, "seed": seed, "png_mode": args.png_mode, "seconds": round(time.perf_counter() - t0, 1),
                             "train_seconds": round(t_train, 1),
                             "first": {k: log[0][k] for k in ("ssim", "bpp", "entropy_loss")},
                             "last20_mean": {k: [float(np.mean([m[k][j] for m in tail])) for j in range(3)]
