@@ -699,11 +699,15 @@ bool use_k3pair() {
   }();
   return on;
 }
-// NIC_K3P=d: the direct (9-tap) fused pair even where the Winograd pair applies (A/B)
+// NIC_K3P=w: the fused pair on Winograd F(2,3) along y where it applies (planes up to 64
+// columns).  Not the default: measured slower than the direct pair (0.304 vs 0.261 ms per
+// launch, same box) -- both layers' U kernels (384 VGPRs per 16 channels)
+// leave one wave per SIMD, so its transform / epilogue VALU (PMC: 4.0 per MFMA) cannot overlap
+// a partner's MFMAs (MFMA busy 0.34 vs 0.71).
 bool use_k3wino() {
   static const bool on = [] {
     const char* e = getenv("NIC_K3P");
-    return use_k3pair() && !(e && e[0] == 'd');
+    return use_k3pair() && e && e[0] == 'w';
   }();
   return on;
 }

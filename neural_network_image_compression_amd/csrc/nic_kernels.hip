@@ -2635,6 +2635,162 @@ __global__ __launch_bounds__(256, 2) void dconv1_ws_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// dconv1 with all four sub-pixel phases per staged tile (round 4; NIC_D1=a, see
+// launch_dconv1_all).  dconv1_ws_kernel walks its tiles once per phase: every tile's 10 x 10
+// halo of codes is loaded and converted to f16 four times (PMC: 96 MB fetched for 6.3 MB of
+// codes) and each pass runs only 32-72 MFMAs per wave between two barriers (VALU : MFMA 5.2,
+// SALU : MFMA 3.1, MFMA busy 0.25).  Here a block of 8 waves (one per CU) stages a tile's
+// codes once and runs all 25 taps on it: wave w < 4 holds phases (1,1) and (0,0) (9 + 4 taps),
+// wave w + 4 phases (0,1) and (1,0) (6 + 6 taps) of output channels 16 (w & 3) .. + 15 -- 13 and
+// 12 taps of resident A fragments (w_hi, w_lo of 32 input channels: 8 VGPRs per tap), so the
+// two SIMD partners carry nearly equal MFMA work on one halo and each phase's epilogue
+// overlaps its partner's MFMAs.  Same MFMA chains and epilogue arithmetic as d1_body: the
+// outputs are bit-identical to dconv1_ws_kernel (GPU test).
+// ------------------------------------------------------------------------------------
+constexpr int D1A_LD = 2;  // code dwords per thread per tile (800 over 512 threads)
+
+template <int KH1, int KW1, int TB1, int PY1, int PX1, int KH2, int KW2, int TB2, int PY2, int PX2>
+__device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
+  constexpr int COUT = 64, MT = 4, TAP_BYTES = 32 * COUT * 4, PXB = COUT * 4;
+  constexpr int NT1 = KH1 * KW1, NT2 = KH2 * KW2;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cg = wave & 3;
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int per_plane = a.tiles_y * a.tiles_x;
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  const int ntot = np * per_plane;
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  if (ntile == 0) return;  // block-uniform
+
+  f16x8 w1[NT1][2], w2[NT2][2];
+  {
+    const char* wsrc = (const char*)a.wx + (size_t)model * 25 * TAP_BYTES;
+    auto frag_w = [&](int tap, int hl) {
+      return *(const f16x8*)(wsrc + (size_t)tap * TAP_BYTES + ((((g >> 1) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
+    };
+#pragma unroll
+    for (int t = 0; t < NT1; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) w1[t][hl] = frag_w(TB1 + t, hl);
+#pragma unroll
+    for (int t = 0; t < NT2; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) w2[t][hl] = frag_w(TB2 + t, hl);
+  }
+  const float scale = a.wscale[model] * 0.0039215688593685627f;  // 2^-k and the dequantiser's 1/255
+  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + cg * 16 + 4 * g);
+
+  // code staging: thread q = threadIdx.x + 512 j loads dword q & 7 of halo pixel q >> 3
+  int st_lds[D1A_LD], st_hy[D1A_LD], st_hx[D1A_LD];
+#pragma unroll
+  for (int j = 0; j < D1A_LD; ++j) {
+    const int q = threadIdx.x + 512 * j, pix = q >> 3;
+    st_hy[j] = q < 800 ? pix / 10 : -1000;
+    st_hx[j] = pix - (pix / 10) * 10;
+    st_lds[j] = (pix / 10) * D1_RPB + st_hx[j] * D1_PSB + (q & 7) * 8;
+  }
+  uint32_t cq[D1A_LD];
+  TileWalk it_ld, it_run;
+  it_ld.init(bi, nb, a.tiles_y, a.tiles_x);
+  it_run = it_ld;
+  auto load_codes = [&] {
+    int pl, ty, tx;
+    it_ld.take(pl, ty, tx);
+    const int p = p0 + pl;
+    const uint8_t* base = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
+#pragma unroll
+    for (int j = 0; j < D1A_LD; ++j) {
+      const int gy = ty * 8 - 1 + st_hy[j], gx = tx * 8 - 1 + st_hx[j];
+      const bool ok = (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+      cq[j] = ok ? *(const uint32_t*)(base + ((size_t)gy * a.W + gx) * 96 + (threadIdx.x & 7) * 4) : 0u;
+    }
+  };
+  const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);
+  const unsigned out_plane = (unsigned)((size_t)a.OH * a.OW * PXB);
+  unsigned g_off[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int dy = 2 * m + (l16 >> 3), dx = l16 & 7;
+    g_off[m] = (unsigned)(((2 * dy) * a.OW + 2 * dx) * PXB + st_off * 2);
+  }
+  float rmax = 0.f;
+  // one phase of the staged tile: MFMA chains over its taps, then bias + leaky + split stores
+  auto phase = [&](const char* buf, const f16x8* wr, auto shape_c, int py, int px, int p, int ty0, int tx0) {
+    constexpr int KH = decltype(shape_c)::value / 4, KW = decltype(shape_c)::value % 4, NTAPS = KH * KW;
+    int bx[KW];
+#pragma unroll
+    for (int kw = 0; kw < KW; ++kw) bx[kw] = (l16 >> 3) * D1_RPB + ((l16 & 7) + kw) * D1_PSB + g * 16;  // halo origin (y - 1, x - 1)
+    const unsigned bb = lds_off(buf);
+    auto frag = [&](int m, int t) {
+      const int kh = t / KW, kw = t - kh * KW;
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(bb + bx[kw]) + (2 * m + kh) * D1_RPB);
+    };
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f16x8 fb[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) fb[m] = frag(m, 0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t + 1], fb[m], acc[m], 0, 0, 0);  // w_lo*c
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t], fb[m], acc[m], 0, 0, 0);      // w_hi*c
+        if (t + 1 < NTAPS) fb[m] = frag(m, t + 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.out_s + (size_t)p * out_plane / 2), (short)0, (int)out_plane, kBufWord3);
+    const unsigned out_org = (unsigned)(((2 * ty0 + py) * a.OW + 2 * tx0 + px) * PXB);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int y = ty0 + 2 * m + (l16 >> 3), x = tx0 + (l16 & 7);
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+      const bool in = y < a.H && x < a.W;
+      if (in) range_track(rmax, v);
+      f16x4 hi, lo;
+      split4(v, hi, lo);
+      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), out_rs, in ? out_org + g_off[m] : kDmaOOR, 0, 0);
+    }
+  };
+  load_codes();
+  for (int i = 0; i < ntile; ++i) {
+    char* buf = lds + (i & 1) * D1_HB;
+#pragma unroll
+    for (int j = 0; j < D1A_LD; ++j) {  // codes -> f16 (exact) in LDS
+      if (st_hy[j] < 0) continue;
+      const uint32_t q = cq[j];
+      const f16x4 c = {(_Float16)(float)(q & 255), (_Float16)(float)((q >> 8) & 255),
+                       (_Float16)(float)((q >> 16) & 255), (_Float16)(float)(q >> 24)};
+      *(f16x4*)(buf + st_lds[j]) = c;
+    }
+    lds_reads_done();
+    stage_barrier();  // tile i's halo complete; tile i-2's reads of this buffer done everywhere
+    int pl, ty, tx;
+    it_run.take(pl, ty, tx);
+    if (i + 1 < ntile) load_codes();  // lands during this tile's MFMAs
+    phase(buf, &w1[0][0], std::integral_constant<int, KH1 * 4 + KW1>{}, PY1, PX1, p0 + pl, ty * 8, tx * 8);
+    phase(buf, &w2[0][0], std::integral_constant<int, KH2 * 4 + KW2>{}, PY2, PX2, p0 + pl, ty * 8, tx * 8);
+  }
+  range_report(a.rg, rmax);
+}
+
+__global__ __launch_bounds__(512, 1) void dconv1_all_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * D1_HB];
+  const int gi = (int)blockIdx.x >= a.ws_blk[1] ? 1 : 0;
+  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  if (threadIdx.x < 256)  // phases (1,1) 3x3 taps (tap base 16) and (0,0) 2x2 (base 0)
+    d1all_wave<3, 3, 16, 1, 1, 2, 2, 0, 0, 0>(a, lds, gi, bi, nb);
+  else  // phases (0,1) 2x3 (base 4) and (1,0) 3x2 (base 10)
+    d1all_wave<2, 3, 4, 0, 1, 3, 2, 10, 1, 0>(a, lds, gi, bi, nb);
+}
+
+// ------------------------------------------------------------------------------------
 // Fused residual pair of the k3 s1 layers: out = leaky(conv_b(leaky(conv_a(x) + b_a)) + b_b) + x
 // (encoder.py:22-25 conv3 -> conv4 -> + res; decoder.py:26-29 dconv5 -> dconv6 -> + res, the
 // Conv2DTranspose k3 s1 layers repacked as flipped convs).  Split-f16 in and out.
@@ -3036,6 +3192,13 @@ constexpr int K3W_ROWB = K3P_ROWB;                  // one V row: records x = -1
 constexpr int K3W_SETB = 4 * K3W_ROWB;              // four V rows (69,632 B)
 constexpr int K3W_STGB = 64 * K3P_REC;              // one raw input row (16,384 B)
 constexpr int K3W_LDS = 2 * K3W_SETB + K3W_STGB;    // 155,648 B
+// the epilogues and the VI build placed inside the next tile's MFMA stream (1) or after it (0;
+// 0.304 vs 0.327 ms per launch on the same box: with one wave per SIMD the interleave only
+// adds live registers, 41 vs 17 spills)
+#ifndef NIC_K3W_IL
+#define NIC_K3W_IL 0
+#endif
+constexpr bool kK3wIL = NIC_K3W_IL != 0;
 
 // a value the compiler must treat as redefined here: keeps loop-invariant addresses (lane
 // constants) from being hoisted out of the step loop and held in VGPRs across it
@@ -3088,7 +3251,9 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
 
   // B fragments: pixel 16 m + l16 at tap column kx -> record 16 m + l16 + kx of a V row; lane
   // group g reads chunk 8 hl + 4 ks + g (the XOR with (2 hl + ks) << 6 selects hl, ks)
-  const unsigned bx0 = (unsigned)k3p_off(l16, g);  // + 256 kx: the swizzle of record l16 + kx
+  unsigned bx[3];  // per tap column: record l16 + kx with its own swizzle
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) bx[kx] = (unsigned)k3p_off(l16 + kx, g);
   const int chunk_st = (g & 1) * 8 + 2 * w + (g >> 1);  // this lane's 16-B granule after swap16_pair
 
   f16x8 wa[12][KST][2], wb[12][KST][2];  // conv_a / conv_b U fragments of channels 16 w ..
@@ -3096,7 +3261,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
   float scale_a = 0.f, scale_b = 0.f;
   f32x4 bias_a = {}, bias_b = {};
   float rmax = 0.f;
-  auto load_weights = [&](int m) {
+  auto load_weights = [&](int m) __attribute__((always_inline)) {
     constexpr int TAP_BYTES = 64 * COUT * 4;
     const char* sa = (const char*)a.wxw + (size_t)m * 12 * TAP_BYTES;
     const char* sb = (const char*)a.wxw2 + (size_t)m * 12 * TAP_BYTES;
@@ -3116,41 +3281,50 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
     bias_b = *(const f32x4*)(a.bias2 + m * COUT + 16 * w + 4 * g);
   };
 
-  // M_xi of pixel tile m over a V set with the U fragments wr (xi-major, 24 steps of 3
-  // MFMAs; B fragments read two steps ahead)
+  // M_xi of pixel tile M over a V set with the U fragments wr (xi-major, 24 steps of 3 MFMAs;
+  // B fragments read two steps ahead) into acc[M & 1]; hook(step) after every step places
+  // the previous tile's epilogue and the VI build in the stream (kK3wIL; the MFMA of one
+  // step and a slice of vector work then issue together -- one wave per SIMD has no partner
+  // whose VALU could fill the MFMA gaps)
   f32x4 acc[4];
-  auto mfma_tile = [&](const char* set, const f16x8 (&wr)[12][KST][2], int m) {
+  auto mfma_tile = [&](const char* set, const f16x8 (&wr)[12][KST][2], auto mc, auto&& hook) __attribute__((always_inline)) {
+    constexpr int M = decltype(mc)::value;
+    f32x4(&ac)[4] = acc;
     __builtin_amdgcn_sched_barrier(0);  // the previous tile's epilogue stays ahead of these reads
-    const unsigned b0 = opaque(lds_off(set) + bx0);
-    auto frag = [&](int st, int hl) {
+    hook(std::integral_constant<int, -1>{});  // before the accumulators restart: the previous tile's sums
+    const unsigned sb = lds_off(set);
+    const unsigned b0[3] = {opaque(sb + bx[0]), opaque(sb + bx[1]), opaque(sb + bx[2])};
+    auto frag = [&](int st, int hl) __attribute__((always_inline)) {
       const int xi = st / (3 * KST), r = st - xi * 3 * KST, kx = r / KST, ks = r - kx * KST;
-      return *(const __attribute__((address_space(3))) f16x8*)(lds_at((b0 + 256u * kx) ^ (unsigned)((2 * hl + ks) << 6)) +
-                                                               xi * K3W_ROWB + m * 16 * K3P_REC);
+      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(b0[kx] ^ (unsigned)((2 * hl + ks) << 6)) +
+                                                               xi * K3W_ROWB + M * 16 * K3P_REC);
     };
     constexpr int NSTEP = 12 * KST, DEPTH = 2;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < 4; ++q) ac[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
     f16x8 fb[DEPTH][2];
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       fb[d][0] = frag(d, 0);
       fb[d][1] = frag(d, 1);
     }
-    static_for<NSTEP>([&](auto stc) {
+    static_for<NSTEP>([&](auto stc) __attribute__((always_inline)) {
       constexpr int st = decltype(stc)::value, xi = st / (3 * KST), t = st / KST, ks = st % KST;
       f16x8(&cur)[2] = fb[st % DEPTH];
-      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], acc[xi], 0, 0, 0);  // u_lo*v_hi
-      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], acc[xi], 0, 0, 0);  // u_hi*v_lo
-      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], acc[xi], 0, 0, 0);  // u_hi*v_hi
+      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], ac[xi], 0, 0, 0);  // u_lo*v_hi
+      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], ac[xi], 0, 0, 0);  // u_hi*v_lo
+      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], ac[xi], 0, 0, 0);  // u_hi*v_hi
       if constexpr (st + DEPTH < NSTEP) {
         cur[0] = frag(st + DEPTH, 0);
         cur[1] = frag(st + DEPTH, 1);
       }
+      hook(stc);
       __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
     });
   };
-  // the pair's two output rows (fp32, before bias) of the tile just computed
-  auto out_transform = [&](f32x4& y0, f32x4& y1) {
+  auto no_hook = [](auto) __attribute__((always_inline)) {};
+  // the pair's two output rows (fp32, before bias) of tile M
+  auto out_transform = [&](f32x4& y0, f32x4& y1) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       y0[r] = __fadd_rn(__fadd_rn(acc[0][r], acc[1][r]), acc[2][r]);
@@ -3159,73 +3333,107 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
   };
   // this lane's granule (chunk_st) of V row xi, record rec, in VB: read as fp32 (hi + lo of
   // its 4 channels) / write split
-  auto vrec = [&](int xi, int rec) { return vb + xi * K3W_ROWB + opaque(k3p_off(rec, chunk_st)); };
-  auto read_v = [&](int xi, int rec) {
-    const u32x4 q = *(const u32x4*)vrec(xi, rec);
+  auto vrec = [&](int xi, int rec) __attribute__((always_inline)) { return vb + xi * K3W_ROWB + opaque(k3p_off(rec, chunk_st)); };
+  auto unpack_v = [&](const u32x4& q) __attribute__((always_inline)) {
     f16x4 hi, lo;
     unswap16(q, hi, lo);
     return unsplit4(hi, lo);
   };
-  auto write_v = [&](int xi, int rec, const f32x4& v) {
+  auto write_v = [&](int xi, int rec, const f32x4& v) __attribute__((always_inline)) {
     range_track(rmax, v);
     f16x4 hi, lo;
     split4(v, hi, lo);
     *(u32x4*)vrec(xi, rec) = swap16_pair(hi, lo);
   };
 
-  // A: conv_a pair (t0, t0 + 1) from VI, then VB for conv_b's pair (t0 - 1, t0) -- or, first
-  // pair of a segment, a VB from which the next build recovers (a(t0), a(t0 + 1))
-  auto a_step = [&](int t0, bool first) {
-    static_for<MT>([&](auto mc) {
-      constexpr int m = decltype(mc)::value;
-      mfma_tile(vi, wa, m);
+  // ---- A epilogue of tile m (conv_a pair (t0, t0 + 1)): VB for conv_b's pair (t0 - 1, t0),
+  // or -- first pair of a segment -- a VB from which the next one recovers (a(t0), a(t0 + 1)).
+  // Pieces 0 .. 6, in order (kK3wIL: spread over the next tile's MFMA steps) ----
+  f32x4 ea0, ea1, ep0, ep1;
+  u32x4 er[3];
+  auto a_epi = [&](int piece, int m, int t0, bool first) __attribute__((always_inline)) {
+    const int x = 16 * m + l16, rec = x + 1;
+    if (piece == 0) {
       f32x4 y0, y1;
       out_transform(y0, y1);
-      const int x = 16 * m + l16, rec = x + 1;
       const bool vx = x < W;
       const bool v0 = vx && (unsigned)t0 < (unsigned)H, v1 = vx && (unsigned)(t0 + 1) < (unsigned)H;
-      f32x4 a0, a1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        a0[r] = v0 ? leaky02(scale_bias(y0[r], scale_a, bias_a[r])) : 0.f;
-        a1[r] = v1 ? leaky02(scale_bias(y1[r], scale_a, bias_a[r])) : 0.f;
+        ea0[r] = v0 ? leaky02(scale_bias(y0[r], scale_a, bias_a[r])) : 0.f;
+        ea1[r] = v1 ? leaky02(scale_bias(y1[r], scale_a, bias_a[r])) : 0.f;
       }
-      if (first) {  // recovers as (p0, p1) = (a0, a1): V1 = V2 = a0, V3 = -a1 (V0 unused)
-        write_v(1, rec, a0);
-        write_v(2, rec, a0);
-        write_v(3, rec, -a1);
-      } else {
-        const f32x4 o1 = read_v(1, rec), o2 = read_v(2, rec), o3 = read_v(3, rec);
-        f32x4 p0, p1;
+    } else if (first) {  // recovers as (p0, p1) = (a0, a1): V1 = V2 = a0, V3 = -a1 (V0 unused)
+      if (piece == 3) write_v(1, rec, ea0);
+      if (piece == 4) write_v(2, rec, ea0);
+      if (piece == 5) write_v(3, rec, -ea1);
+    } else if (piece == 1) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          p0[r] = __fmul_rn(__fadd_rn(o1[r], o2[r]), 0.5f);                       // a(t0 - 2)
-          p1[r] = __fsub_rn(__fmul_rn(__fsub_rn(o1[r], o2[r]), 0.5f), o3[r]);     // a(t0 - 1)
-        }
-        f32x4 n;
+      for (int k = 0; k < 3; ++k) er[k] = *(const u32x4*)vrec(k + 1, rec);
+    } else if (piece == 2) {
+      const f32x4 o1 = unpack_v(er[0]), o2 = unpack_v(er[1]), o3 = unpack_v(er[2]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(p0[r], a0[r]);
-        write_v(0, rec, n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) n[r] = __fadd_rn(p1[r], a0[r]);
-        write_v(1, rec, n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(a0[r], p1[r]);
-        write_v(2, rec, n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) n[r] = __fsub_rn(p1[r], a1[r]);
-        write_v(3, rec, n);
+      for (int r = 0; r < 4; ++r) {
+        ep0[r] = __fmul_rn(__fadd_rn(o1[r], o2[r]), 0.5f);                    // a(t0 - 2)
+        ep1[r] = __fsub_rn(__fmul_rn(__fsub_rn(o1[r], o2[r]), 0.5f), o3[r]);  // a(t0 - 1)
       }
-    });
+    } else {
+      const int xi = piece - 3;
+      f32x4 n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        n[r] = xi == 0 ? __fsub_rn(ep0[r], ea0[r]) : xi == 1 ? __fadd_rn(ep1[r], ea0[r])
+             : xi == 2 ? __fsub_rn(ea0[r], ep1[r]) : __fsub_rn(ep1[r], ea1[r]);
+      write_v(xi, rec, n);
+    }
   };
+  constexpr int A_PIECES = 7;
 
-  // VI for conv_a's pair with input rows d0 = y0 .. d3 = y0 + 3: lane (g, l16) of wave w takes
-  // pixel 16 w + l16 (w < MT) and channel chunks g, 4 + g (B-fragment order: conflict-free
-  // reads), each in two halves of 4 channels; d2 from the prefetch registers, d3 from the
-  // staging row, d0 / d1 recovered from the VI being replaced -- or, first pair of a segment
-  // (FIRST), all four rows from HBM
-  u32x4 pf[2][2];  // the d2 prefetch: [item ks][hi, lo]
-  auto load_item = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int ks, u32x4 (&q)[2]) {
+  // ---- B epilogue of tile m (conv_b pair (y, y + 1)): + residual (input rows y, y + 1, loaded
+  // into res[m & 1] when the tile starts), split stores.  Pieces 0 .. 3 ----
+  u32x4 res[2];
+  f32x4 eq0, eq1;
+  auto b_res_load = [&](const __amdgpu_buffer_rsrc_t& rs_in, int m, int y) __attribute__((always_inline)) {
+    const int x = 16 * m + l16;
+    const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
+    const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
+    res[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v0 ? o0 : kDmaOOR, 0, 0));
+    res[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs_in, v1 ? o0 + (unsigned)(W * K3P_REC) : kDmaOOR, 0, 0));
+  };
+  auto b_epi = [&](int piece, int m, int y, const __amdgpu_buffer_rsrc_t& rs_out) __attribute__((always_inline)) {
+    const int x = 16 * m + l16;
+    const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
+    if (piece == 0) {
+      f32x4 y0, y1;
+      out_transform(y0, y1);
+      const f32x4 x0 = unpack_v(res[0]), x1 = unpack_v(res[1]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // x = x + res (encoder.py:25, decoder.py:29)
+        eq0[r] = __fadd_rn(leaky02(scale_bias(y0[r], scale_b, bias_b[r])), x0[r]);
+        eq1[r] = __fadd_rn(leaky02(scale_bias(y1[r], scale_b, bias_b[r])), x1[r]);
+      }
+    } else {
+      const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
+      const f32x4 q = piece == 1 ? eq0 : eq1;
+      const bool v = piece == 1 ? v0 : v1;
+      if (v) range_track(rmax, q);
+      f16x4 hi, lo;
+      split4(q, hi, lo);
+      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out,
+                                             v ? o0 + (piece == 1 ? 0u : (unsigned)(W * K3P_REC)) : kDmaOOR, 0, 0);
+    }
+  };
+  constexpr int B_PIECES = 3;
+
+  // ---- VI for conv_a's pair with input rows d0 = y0 .. d3 = y0 + 3.  Lane (g, l16) of wave w
+  // takes pixel 16 w + l16 (w < MT) and channel chunks g, 4 + g (B-fragment order: conflict-free
+  // reads), each in two halves of 4 channels (half-items k = 2 ks + h); d2 from the prefetch
+  // registers, d3 from the staging row, d0 / d1 recovered from the VI being replaced -- or,
+  // first pair of a segment (FIRST), all four rows from HBM.  Pieces 0 .. 5 per half-item ----
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x4 pf[2][2];  // row d3 of the VI build: [item ks][hi, lo]
+  auto load_item = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int ks, u32x4 (&q)[2]) __attribute__((always_inline)) {
     const int x = 16 * w + l16;
     const bool ok = w < MT && (unsigned)y < (unsigned)H && x < W;
 #pragma unroll
@@ -3234,68 +3442,92 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
       q[hl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
   };
-  auto build_vi = [&](const __amdgpu_buffer_rsrc_t& rs, int y0, auto first_c) {
-    constexpr bool FIRST = decltype(first_c)::value;
+  auto unsplit2x2 = [&](u32x2 hi, u32x2 lo, float (&o)[4]) __attribute__((always_inline)) {
+    o[0] = add_f16_pair<0>(hi[0], lo[0]);
+    o[1] = add_f16_pair<1>(hi[0], lo[0]);
+    o[2] = add_f16_pair<0>(hi[1], lo[1]);
+    o[3] = add_f16_pair<1>(hi[1], lo[1]);
+  };
+  u32x2 bq[4][2];  // raw reads of a half-item: V1', V2', V3', d3 [hi, lo]; then its new V rows
+  auto vi_at = [&](const char* base, int r, int c, int h, int hl) __attribute__((always_inline)) {
+    return base + opaque(k3p_off(r, 8 * hl + c)) + 8 * h;
+  };
+  auto build_piece = [&](int piece, int k) __attribute__((always_inline)) {  // steady state (not FIRST): pieces 0 .. 5
+    const int ks = k >> 1, h = k & 1, c = 4 * ks + g, x = 16 * w + l16, rec = x + 1;
+    auto half_of = [&](const u32x4& q) __attribute__((always_inline)) { return (u32x2){q[2 * h], q[2 * h + 1]}; };
+    if (piece == 0) {
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+        for (int xi = 1; xi <= 3; ++xi) bq[xi - 1][hl] = *(const u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, hl);
+        bq[3][hl] = *(const u32x2*)vi_at(stg, x, c, h, hl);  // staging record = x (row d2)
+      }
+    } else if (piece == 1) {  // the four new V rows, split in place of the raw reads
+      float v1[4], v2[4], v3[4], d0[4], d1[4], d2[4], d3[4];
+      unsplit2x2(bq[0][0], bq[0][1], v1);
+      unsplit2x2(bq[1][0], bq[1][1], v2);
+      unsplit2x2(bq[2][0], bq[2][1], v3);
+      unsplit2x2(bq[3][0], bq[3][1], d2);                       // staging: row d2
+      unsplit2x2(half_of(pf[ks][0]), half_of(pf[ks][1]), d3);  // registers: row d3
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        d0[e] = __fmul_rn(__fadd_rn(v1[e], v2[e]), 0.5f);                    // d2 of the old pair
+        d1[e] = __fsub_rn(__fmul_rn(__fsub_rn(v1[e], v2[e]), 0.5f), v3[e]);  // its d3
+      }
+#pragma unroll
+      for (int xi = 0; xi < 4; ++xi) {
+        f32x4 n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          n[e] = xi == 0 ? __fsub_rn(d0[e], d2[e]) : xi == 1 ? __fadd_rn(d1[e], d2[e])
+               : xi == 2 ? __fsub_rn(d2[e], d1[e]) : __fsub_rn(d1[e], d3[e]);
+        range_track(rmax, n);
+        f16x4 hi, lo;
+        split4(n, hi, lo);
+        bq[xi][0] = __builtin_bit_cast(u32x2, hi);
+        bq[xi][1] = __builtin_bit_cast(u32x2, lo);
+      }
+    } else {
+      const int xi = piece - 2;
+      *(u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 0) = bq[xi][0];
+      *(u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 1) = bq[xi][1];
+    }
+  };
+  constexpr int BUILD_PIECES = 6;
+  auto build_vi_first = [&](const __amdgpu_buffer_rsrc_t& rs, int y0) __attribute__((always_inline)) {  // a segment's prologue
     if (w >= MT) return;  // wave-uniform
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const int x = 16 * w + l16, rec = x + 1;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = 4 * ks + g;
-      u32x4 q0[2], q1[2], q3[2];
-      if constexpr (FIRST) {  // a segment's prologue: latency exposed once per segment
-        load_item(rs, y0, ks, q0);
-        load_item(rs, y0 + 1, ks, q1);
-        load_item(rs, y0 + 2, ks, pf[ks]);
-        load_item(rs, y0 + 3, ks, q3);
-      }
+      u32x4 q[4][2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) load_item(rs, y0 + r, ks, q[r]);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        auto at = [&](const char* base, int r, int hl) { return base + opaque(k3p_off(r, 8 * hl + c)) + 8 * h; };
-        auto unsplit2x2 = [&](u32x2 hi, u32x2 lo, float (&o)[4]) {
-          o[0] = add_f16_pair<0>(hi[0], lo[0]);
-          o[1] = add_f16_pair<1>(hi[0], lo[0]);
-          o[2] = add_f16_pair<0>(hi[1], lo[1]);
-          o[3] = add_f16_pair<1>(hi[1], lo[1]);
-        };
-        auto half_of = [&](const u32x4& q) { return (u32x2){q[2 * h], q[2 * h + 1]}; };
-        float d0[4], d1[4], d2[4], d3[4];
-        unsplit2x2(half_of(pf[ks][0]), half_of(pf[ks][1]), d2);
-        if constexpr (FIRST) {
-          unsplit2x2(half_of(q0[0]), half_of(q0[1]), d0);
-          unsplit2x2(half_of(q1[0]), half_of(q1[1]), d1);
-          unsplit2x2(half_of(q3[0]), half_of(q3[1]), d3);
-        } else {
-          unsplit2x2(*(const u32x2*)at(stg, x, 0), *(const u32x2*)at(stg, x, 1), d3);  // staging record = x
-          float v1[4], v2[4], v3[4];
-          unsplit2x2(*(const u32x2*)at(vi + K3W_ROWB, rec, 0), *(const u32x2*)at(vi + K3W_ROWB, rec, 1), v1);
-          unsplit2x2(*(const u32x2*)at(vi + 2 * K3W_ROWB, rec, 0), *(const u32x2*)at(vi + 2 * K3W_ROWB, rec, 1), v2);
-          unsplit2x2(*(const u32x2*)at(vi + 3 * K3W_ROWB, rec, 0), *(const u32x2*)at(vi + 3 * K3W_ROWB, rec, 1), v3);
+        auto half_of = [&](const u32x4& v) __attribute__((always_inline)) { return (u32x2){v[2 * h], v[2 * h + 1]}; };
+        float d[4][4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            d0[e] = __fmul_rn(__fadd_rn(v1[e], v2[e]), 0.5f);                    // d2 of the old pair
-            d1[e] = __fsub_rn(__fmul_rn(__fsub_rn(v1[e], v2[e]), 0.5f), v3[e]);  // its d3
-          }
-        }
+        for (int r = 0; r < 4; ++r) unsplit2x2(half_of(q[r][0]), half_of(q[r][1]), d[r]);
 #pragma unroll
         for (int xi = 0; xi < 4; ++xi) {
           f32x4 n;
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            n[e] = xi == 0 ? __fsub_rn(d0[e], d2[e]) : xi == 1 ? __fadd_rn(d1[e], d2[e])
-                 : xi == 2 ? __fsub_rn(d2[e], d1[e]) : __fsub_rn(d1[e], d3[e]);
+            n[e] = xi == 0 ? __fsub_rn(d[0][e], d[2][e]) : xi == 1 ? __fadd_rn(d[1][e], d[2][e])
+                 : xi == 2 ? __fsub_rn(d[2][e], d[1][e]) : __fsub_rn(d[1][e], d[3][e]);
           range_track(rmax, n);
           f16x4 hi, lo;
           split4(n, hi, lo);
-          *(f16x4*)at(vi + xi * K3W_ROWB, rec, 0) = hi;
-          *(f16x4*)at(vi + xi * K3W_ROWB, rec, 1) = lo;
+          *(f16x4*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 0) = hi;
+          *(f16x4*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 1) = lo;
         }
       }
     }
   };
 
   // the staging DMA of input row y (records 0 .. 63, chunk k of record r in slot k ^ (2r & 15))
-  auto dma_stage = [&](const __amdgpu_buffer_rsrc_t& rs, int y) {
+  auto dma_stage = [&](const __amdgpu_buffer_rsrc_t& rs, int y) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = w; k < 16; k += 4) {  // 16 pieces of 1 KB
       const int q = 64 * k + lane, rec = q >> 4, ch = (q & 15) ^ ((2 * rec) & 15);
@@ -3303,38 +3535,58 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
       dma16_buf(rs, ok ? (unsigned)((y * W + rec) * K3P_REC + ch * 16) : kDmaOOR, stg + k * 1024);
     }
   };
-  // B: conv_b pair (y, y + 1) from VB, + residual (input rows y, y + 1), split stores
-  auto b_step = [&](const __amdgpu_buffer_rsrc_t& rs_in, const __amdgpu_buffer_rsrc_t& rs_out, int y) {
-    static_for<MT>([&](auto mc) {
+
+  // A-step: conv_a pair (t0, t0 + 1) from VI, its epilogue into VB
+  auto a_step = [&](int t0, auto first_c) __attribute__((always_inline)) {
+    constexpr bool first = decltype(first_c)::value;
+    static_for<MT>([&](auto mc) __attribute__((always_inline)) {
       constexpr int m = decltype(mc)::value;
-      const int x = 16 * m + l16;
-      const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
-      const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
-      const unsigned o1 = o0 + (unsigned)(W * K3P_REC);
-      const u32x4 r0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v0 ? o0 : kDmaOOR, 0, 0));
-      const u32x4 r1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v1 ? o1 : kDmaOOR, 0, 0));
-      mfma_tile(vb, wb, m);
-      f32x4 y0, y1;
-      out_transform(y0, y1);
-      f16x4 rh, rl;
-      unswap16(r0, rh, rl);
-      const f32x4 x0 = unsplit4(rh, rl);
-      unswap16(r1, rh, rl);
-      const f32x4 x1 = unsplit4(rh, rl);
-      f32x4 q0, q1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {  // x = x + res (encoder.py:25, decoder.py:29)
-        q0[r] = __fadd_rn(leaky02(scale_bias(y0[r], scale_b, bias_b[r])), x0[r]);
-        q1[r] = __fadd_rn(leaky02(scale_bias(y1[r], scale_b, bias_b[r])), x1[r]);
+      if constexpr (kK3wIL && m > 0) {  // tile m - 1's epilogue inside tile m's stream
+        mfma_tile(vi, wa, mc, [&](auto stc) __attribute__((always_inline)) {
+          constexpr int st = decltype(stc)::value;
+          if constexpr (st == -1) a_epi(0, m - 1, t0, first);  // the sums, before acc restarts
+          if constexpr (st >= 0 && st % 3 == 0 && st / 3 + 1 < A_PIECES) a_epi(st / 3 + 1, m - 1, t0, first);
+        });
+      } else {
+        mfma_tile(vi, wa, mc, no_hook);
+        if constexpr (!kK3wIL) static_for<A_PIECES>([&](auto pc) __attribute__((always_inline)) { a_epi(decltype(pc)::value, m, t0, first); });
       }
-      if (v0) range_track(rmax, q0);
-      if (v1) range_track(rmax, q1);
-      f16x4 hi, lo;
-      split4(q0, hi, lo);
-      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out, v0 ? o0 : kDmaOOR, 0, 0);
-      split4(q1, hi, lo);
-      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out, v1 ? o1 : kDmaOOR, 0, 0);
     });
+    if constexpr (kK3wIL) static_for<A_PIECES>([&](auto pc) __attribute__((always_inline)) { a_epi(decltype(pc)::value, MT - 1, t0, first); });
+  };
+  // B-step: conv_b pair (y, y + 1) from VB (+ residual, stores); with `build`, the VI of the
+  // next conv_a pair (in place, half-item m in tile m's stream when MT = 4)
+  auto b_step = [&](const __amdgpu_buffer_rsrc_t& rs_in, const __amdgpu_buffer_rsrc_t& rs_out, int y, auto conv_c,
+                    auto build_c) __attribute__((always_inline)) {
+    constexpr bool conv = decltype(conv_c)::value, build = decltype(build_c)::value;
+    constexpr bool IL_BUILD = kK3wIL && MT == 4;
+    if constexpr (conv) {
+      static_for<MT>([&](auto mc) __attribute__((always_inline)) {
+        constexpr int m = decltype(mc)::value;
+        if constexpr (kK3wIL) {
+          mfma_tile(vb, wb, mc, [&](auto stc) __attribute__((always_inline)) {
+            constexpr int st = decltype(stc)::value;
+            if constexpr (st == -1) {  // the previous tile's sums + residual, then this tile's residual loads
+              if constexpr (m > 0) b_epi(0, m - 1, y, rs_out);
+              b_res_load(rs_in, m, y);
+            }
+            if constexpr (m > 0 && st >= 0 && st % 2 == 0 && st / 2 + 1 < B_PIECES) b_epi(st / 2 + 1, m - 1, y, rs_out);
+            if constexpr (build && IL_BUILD && st >= 6 && (st - 6) % 3 == 0 && (st - 6) / 3 < BUILD_PIECES)
+              build_piece((st - 6) / 3, m);
+          });
+        } else {
+          b_res_load(rs_in, m, y);
+          mfma_tile(vb, wb, mc, no_hook);
+          static_for<B_PIECES>([&](auto pc) __attribute__((always_inline)) { b_epi(decltype(pc)::value, m, y, rs_out); });
+        }
+      });
+      if constexpr (kK3wIL) static_for<B_PIECES>([&](auto pc) __attribute__((always_inline)) { b_epi(decltype(pc)::value, MT - 1, y, rs_out); });
+    }
+    if constexpr (build && (!IL_BUILD || !conv))
+      if (w < MT)
+        static_for<4>([&](auto k) __attribute__((always_inline)) {
+        static_for<BUILD_PIECES>([&](auto pc) __attribute__((always_inline)) { build_piece(decltype(pc)::value, decltype(k)::value); });
+      });
   };
 
   for (long long gs = g0; gs < g1;) {
@@ -3353,27 +3605,35 @@ __global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
         (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
     // prologue: VI of P_0 (input rows r0 - 2 .. r0 + 1); the previous segment's last conv_b
     // pair has read VB and its stores are in flight
-    build_vi(rs_in, r0 - 2, std::true_type{});
+    build_vi_first(rs_in, r0 - 2);
     lds_reads_done();
     stage_barrier();
-    for (int i = 0; i <= K; ++i) {
-      // A: conv_a pair P_i from VI -> VB (Q_{i-1}); the staging DMA and the d2 prefetch of the
-      // next VI build are issued first so they land during the MFMAs
-      if (i < K) {
-        dma_stage(rs_in, r0 + 2 * i + 3);
-        load_item(rs_in, r0 + 2 * i + 2, 0, pf[0]);
-        load_item(rs_in, r0 + 2 * i + 2, 1, pf[1]);
-      }
-      a_step(r0 + 2 * i - 1, i == 0);
-      dma_wait_all();  // this wave's staging pieces (other waves' lanes read them) and prefetch
+    // step i (0 <= i <= K), the first and last peeled so that every branch of a step is resolved
+    // at compile time (none inside the MFMA streams)
+    auto step = [&](int i, auto first_c, auto conv_c, auto build_c) __attribute__((always_inline)) {
+      constexpr bool build = decltype(build_c)::value;
+      // A: conv_a pair P_i from VI -> VB (Q_{i-1}); the staging DMA of the next VI build's row
+      // d2 is issued first so it lands during the MFMAs
+      if constexpr (build) dma_stage(rs_in, r0 + 2 * i + 2);
+      a_step(r0 + 2 * i - 1, first_c);
+      dma_wait_all();  // this wave's staging pieces (other waves' lanes read them)
       lds_reads_done();
       stage_barrier();  // VB of Q_{i-1} and the staging row complete; every wave's VI reads done
-      // B: conv_b pair Q_{i-1} from VB, then the VI of P_{i+1} (in place)
-      if (i >= 1) b_step(rs_in, rs_out, r0 + 2 * i - 2);
-      if (i < K) build_vi(rs_in, r0 + 2 * i, std::false_type{});
+      // B: conv_b pair Q_{i-1} from VB, and the VI of P_{i+1} (in place; its row d3 loaded now,
+      // used late in the step)
+      if constexpr (build) {
+        load_item(rs_in, r0 + 2 * i + 3, 0, pf[0]);
+        load_item(rs_in, r0 + 2 * i + 3, 1, pf[1]);
+      }
+      b_step(rs_in, rs_out, r0 + 2 * i - 2, conv_c, build_c);
       lds_reads_done();
       stage_barrier();  // VI of P_{i+1} complete; every wave's VB reads done
-    }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    step(0, T_{}, F_{}, T_{});
+    for (int i = 1; i < K; ++i) step(i, F_{}, T_{}, T_{});
+    step(K, F_{}, T_{}, F_{});
   }
   range_report(a.rg, rmax);
 }
@@ -4914,11 +5174,14 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
 }
 
 static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st);
+static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st);
 static int dconv1_variant() {
   static const int v = [] {
     const char* e = getenv("NIC_D1");
-    return !e ? 0 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5
-                  : e[0] == '8' ? 6 : e[0] == 'x' ? 7 : 0;
+    // default: all phases per staged tile (dconv1_all_kernel, 0.056-0.057 vs 0.064-0.065 ms for
+    // the per-phase weight-stationary walk, NIC_D1=p, same box: profiles/r4c_*)
+    return !e ? 8 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5
+                  : e[0] == '8' ? 6 : e[0] == 'x' ? 7 : e[0] == 'a' ? 8 : 0;
   }();
   return v;
 }
@@ -4939,8 +5202,9 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
                    // quarters, 4x8 tiles), or 4x8 tile with taps split over 4 waves
       if (use_ws()) return launch_ws2<64, 32, 4, 4, OUT_U8_LATENT>(a, st);
       return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_SPLIT, OUT_U8_LATENT, false>(a, st);
-    case L_DCONV1:  // latent -> 64, transposed k5 s2: 8x8 coarse tile, 2 waves split N (NIC_D1 A/B:
-                    // "16" 8x16 tile, 2 waves x 4 M tiles; "w4" 8x16 tile, 4 waves)
+    case L_DCONV1:  // latent -> 64, transposed k5 s2: all four phases per staged 8x16 code tile
+                    // (dconv1_all_kernel); NIC_D1=p the per-phase weight-stationary walk, and the
+                    // older one-tile-per-block forms below (A/B)
       switch (dconv1_variant()) {
         case 1: return launch_x3<32, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_U8_CODES, OUT_SPLIT, false>(a, st);
         case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
@@ -4954,6 +5218,7 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
         // epilogue; NIC_D1=s the split dequantised activations, 3 MFMAs, round 2) on 8x16
         // coarse tiles, 4 waves, one tile per block (round-3 default before dconv1_ws_kernel)
         case 7: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
+        case 8: return launch_dconv1_all(a, st);
         default: return launch_dconv1_ws(a, st);
       }
     case L_DCONV5:
@@ -5027,6 +5292,26 @@ static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st) {
   a.ws_blk[1] = by;
   a.ws_blk[2] = by + bc;
   hipLaunchKernelGGL(dconv1_ws_kernel, dim3(by + bc), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// all phases per staged tile: one 8-wave block per CU, blocks split between the models in
+// proportion to their tiles (Y : CbCr = 1 : 2)
+static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
+  a.tiles_y = (a.H + 7) / 8;
+  a.tiles_x = (a.W + 7) / 8;
+  const long long per_plane = (long long)a.tiles_y * a.tiles_x, nt = per_plane * a.P;
+  if (nt == 0) return hipSuccess;
+  if (nt > INT32_MAX || a.P != 3 * a.nimg || a.OH != 2 * a.H || a.OW != 2 * a.W || !a.in_u8) return hipErrorInvalidValue;
+  if ((long long)a.OH * a.OW * 256 >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit granule offsets
+  const long long target = device_cus();
+  const long long ty = (long long)a.nimg * per_plane, tc = 2LL * a.nimg * per_plane;
+  const int by = (int)std::max(1LL, std::min(ty, (target + 1) / 3)), bc = (int)std::max(1LL, std::min(tc, target - by));
+  a.ws_ngrp = 2;
+  a.ws_blk[0] = 0;
+  a.ws_blk[1] = by;
+  a.ws_blk[2] = by + bc;
+  hipLaunchKernelGGL(dconv1_all_kernel, dim3(by + bc), dim3(512), 0, st, a);
   return hipGetLastError();
 }
 

@@ -556,20 +556,22 @@ def _alt_child(tmp_path, switches, tag):
 
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
-                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0", "NIC_K3P": "d"}, {"NIC_K3P": "d"},
-                                      {"NIC_D1": "x"}],
-                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "k3-direct",
-                              "dconv1-tile"])
+                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
+                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}],
+                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep",
+                              "dconv1-tile", "dconv1-perphase"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
-    NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the direct
-    (9-tap) fused k3 pair (NIC_K3P=d), the k3 layers as two launches (NIC_K3P=0) ... meet the
-    golden contract too; they run in a child process because the switches are read when
-    the library loads."""
+    NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the k3 layers
+    as two launches (NIC_K3P=0) or the fused pair in lockstep order, the per-phase dconv1
+    walk (NIC_D1=p) ... meet the golden contract too; they run in a child process because the
+    switches are read when the library loads."""
     dump = _alt_child(tmp_path, switches, "v")
-    if switches == {"NIC_D8G": "l"}:
-        # the LDS-staged gather sums the same projections in the same order as the direct one:
-        # bit-identical to the default
+    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}):
+        # the LDS-staged gather sums the same projections in the same order as the direct one;
+        # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue; the
+        # default (direct 9-tap) fused k3 residual pair runs the same chains and epilogues as
+        # the two weight-stationary launches, in either step order: bit-identical to the default
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from alt_kernels_check import alt_cases
 
@@ -580,26 +582,18 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
         with np.load(dump) as other:
             for k, v in mine.items():
                 np.testing.assert_array_equal(v.cpu().numpy(), other[k], err_msg=k)
-    if switches in ({"NIC_K3P": "0"}, {"NIC_K3P_SK": "0", "NIC_K3P": "d"}):
-        # the direct fused k3 residual pair runs the same MFMA chains and epilogues as the two
-        # weight-stationary launches (in either step order): bit-identical to NIC_K3P=d (the
-        # default Winograd pair is held to the oracle contract instead: test_k3_wino_*)
-        ref = _alt_child(tmp_path, {"NIC_K3P": "d"}, "d")
-        with np.load(dump) as a, np.load(ref) as b:
-            for k in b.files:
-                np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 def test_k3_wino_against_direct_pair(tmp_path, weights_spread):
-    """The default k3 pair (Winograd F(2,3) along y, planes up to 64 columns) against the
-    direct 9-tap pair (NIC_K3P=d, child process) on the alt_kernels_check cases: codes and
+    """The Winograd F(2,3)-along-y k3 pair (NIC_K3P=w, planes up to 64 columns; child process)
+    against the default direct 9-tap pair on the alt_kernels_check cases: codes and
     reconstructions within the oracle contract of each other, pre-quant latents within
     PREQUANT_ATOL (both are within it of the float64 oracle); the max differences are printed."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from alt_kernels_check import alt_cases
 
     from neural_network_image_compression_amd.codec import Codec
-    ref = _alt_child(tmp_path, {"NIC_K3P": "d"}, "d")
+    ref = _alt_child(tmp_path, {"NIC_K3P": "w"}, "w")
     c = Codec(0, precision="f16x3")
     c.set_weights(weights_spread)
     mine = {k: v.cpu().numpy() for k, v in alt_cases(c).items()}
