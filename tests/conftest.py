@@ -43,14 +43,29 @@ def weights_glorot():
     return W.seeded_weights(0, init="glorot")
 
 
-@pytest.fixture(scope="session")
-def weights_trained():
-    """The coefficient-0.01 codec trained for 30 epochs on the reference's 19,000 patches
-    (tools/train_rd.py, round 3), committed under tests/golden/trained."""
-    import os
+TRAINED_COEFS = ("0.01", "0.02", "0.03")
 
+
+def trained_weights(coef="0.01"):
+    """A codec trained for 30 epochs on the reference's 19,000 patches with entropy_loss_coef
+    `coef` (tools/train_rd.py, TF encode_png target, seed 0, round 4), committed under
+    tests/golden/trained."""
     from neural_network_image_compression_amd import weights as W
-    pre = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trained", "coef0.01_")
+    pre = os.path.join(GOLDEN, "trained", f"coef{coef}_")
     w = W.load(pre + "encoder", "encoder")
     w.update(W.load(pre + "decoder", "decoder"))
     return w
+
+
+@pytest.fixture(scope="session")
+def weights_trained():
+    return trained_weights("0.01")
+
+
+@pytest.fixture(scope="session")
+def weights_by_init(weights_spread, weights_glorot, weights_trained):
+    """Every committed weight set by the manifest's "init" name."""
+    out = {"spread": weights_spread, "glorot": weights_glorot, "trained_coef0.01": weights_trained}
+    for c in TRAINED_COEFS[1:]:
+        out[f"trained_coef{c}"] = trained_weights(c)
+    return out

@@ -9,8 +9,9 @@ Inputs come from the reference's own data files (read here as pixel data only):
   * kodim21.png crop [0:256, 0:256] with Keras glorot/zero-bias weights -> 'kodim21_glorot'
   * the whole kodim21.png (512 x 768)          -> case 'kodim21_full'  (BASELINE config 4, whole)
   * its six 256^2 tiles (2 rows x 3 columns)  -> case 'kodim21_tiles' (config 4, tiled)
-  * kodim21_256 and imagenet4 with the TRAINED coefficient-0.01 codec (tests/golden/trained,
-    tools/train_rd.py) -> cases '*_trained'   (--only-trained)
+  * kodim21_256 and imagenet4 with the TRAINED codecs of coefficients 0.01 / 0.02 / 0.03
+    (tests/golden/trained, tools/train_rd.py) -> cases '*_trained', '*_trained_c0.02',
+    '*_trained_c0.03'   (--only-trained)
 The decoded pixels are stored, so the GPU box never decodes JPEG/PNG.
 
 Outputs (oracle, float64-accumulated convolutions): u8 latent, fp32 clipped pre-quant
@@ -89,39 +90,48 @@ def full_resolution_cases(ref_data: str, w, manifest):
         print(name, manifest["cases"][name])
 
 
-TRAINED = os.path.join(OUT, "trained", "coef0.01_")  # + {encoder,decoder}{Y,CbCr}.safetensors
+TRAINED = os.path.join(OUT, "trained")  # coef<c>_{encoder,decoder}{Y,CbCr}.safetensors
+TRAINED_COEFS = ("0.01", "0.02", "0.03")
 
 
-def trained_weights():
-    """The coefficient-0.01 codec trained by tools/train_rd.py (30 epochs over the reference's
-    19,000 patches, round 3, profiles/r3e_train_rd.json), committed as safetensors."""
-    w = W.load(TRAINED + "encoder", "encoder")
-    w.update(W.load(TRAINED + "decoder", "decoder"))
+def trained_weights(coef="0.01"):
+    """A codec trained by tools/train_rd.py with entropy_loss_coef `coef` (30 epochs over the
+    reference's 19,000 patches, the TF encode_png target, seed 0; round 4,
+    profiles/r4t0_train_rd.json), committed as safetensors."""
+    pre = os.path.join(TRAINED, f"coef{coef}_")
+    w = W.load(pre + "encoder", "encoder")
+    w.update(W.load(pre + "decoder", "decoder"))
     return w
+
+
+def trained_case_name(base, coef):
+    return f"{base}_trained" + ("" if coef == "0.01" else f"_c{coef}")
 
 
 def trained_cases(ref_data: str, manifest):
     """Golden vectors with trained weights (realistic activation ranges and latent statistics):
-    the kodim21 crop [0:256, 0:256] and the four ImageNet patches."""
-    w = trained_weights()
-    manifest["weights"]["trained_coef0.01"] = W.digest(w)
-    for name, (x, _) in load_inputs(ref_data).items():
-        if name not in ("kodim21_256", "imagenet4"):
-            continue
-        x = np.ascontiguousarray(x, dtype=np.uint8)
-        f = O.encode_f32(w, x)
-        z = O.quantise_u8(f)
-        rf = O.decode_f32(w, z)
-        r = O.quantise_u8(rf)
-        np.savez_compressed(os.path.join(OUT, f"{name}_trained.npz"), x=x, latent=z, prequant=f, recon=r,
-                            counts=O.histograms(z).astype(np.int32), bits=O.hist_entropy(z))
-        manifest["cases"][name + "_trained"] = {
-            "init": "trained_coef0.01", "x_shape": list(x.shape), "latent_shape": list(z.shape),
-            "recon_shape": list(r.shape), "psnr_db": O.psnr(x, r), "zero_codes": float(np.mean(z == 0)),
-            "bits_mean": float(O.hist_entropy(z).mean()), "codes_near_half": int(near_half(f).sum()),
-            "prequant_absmax": float(np.abs(f).max()),
-        }
-        print(name + "_trained", manifest["cases"][name + "_trained"])
+    the kodim21 crop [0:256, 0:256] and the four ImageNet patches, per trained coefficient."""
+    for coef in TRAINED_COEFS:
+        w = trained_weights(coef)
+        manifest["weights"][f"trained_coef{coef}"] = W.digest(w)
+        for name, (x, _) in load_inputs(ref_data).items():
+            if name not in ("kodim21_256", "imagenet4"):
+                continue
+            x = np.ascontiguousarray(x, dtype=np.uint8)
+            f = O.encode_f32(w, x)
+            z = O.quantise_u8(f)
+            rf = O.decode_f32(w, z)
+            r = O.quantise_u8(rf)
+            case = trained_case_name(name, coef)
+            np.savez_compressed(os.path.join(OUT, f"{case}.npz"), x=x, latent=z, prequant=f, recon=r,
+                                counts=O.histograms(z).astype(np.int32), bits=O.hist_entropy(z))
+            manifest["cases"][case] = {
+                "init": f"trained_coef{coef}", "x_shape": list(x.shape), "latent_shape": list(z.shape),
+                "recon_shape": list(r.shape), "psnr_db": O.psnr(x, r), "zero_codes": float(np.mean(z == 0)),
+                "bits_mean": float(O.hist_entropy(z).mean()), "codes_near_half": int(near_half(f).sum()),
+                "prequant_absmax": float(np.abs(f).max()),
+            }
+            print(case, manifest["cases"][case])
 
 
 def main():

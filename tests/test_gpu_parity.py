@@ -38,12 +38,13 @@ def _dev(a):
 
 
 @pytest.fixture(scope="module", params=["f16x3", "fp32"])
-def codecs(request, weights_spread, weights_glorot, weights_trained):
+def codecs(request, weights_by_init):
     """Both arithmetic modes of the Cin>=32 convolutions must meet the same contract, with
-    seeded weights (spread / Keras glorot) and with the trained coefficient-0.01 codec."""
+    seeded weights (spread / Keras glorot) and with the trained codecs (coefficients 0.01,
+    0.02, 0.03)."""
     from neural_network_image_compression_amd.codec import Codec
     out = {}
-    for name, w in (("spread", weights_spread), ("glorot", weights_glorot), ("trained_coef0.01", weights_trained)):
+    for name, w in weights_by_init.items():
         out[name] = Codec(0, precision=request.param)
         out[name].set_weights(w)
     assert out["spread"].ready() == (True, True) and out["spread"].precision == request.param
@@ -78,7 +79,9 @@ def check_recon(r_gpu, r_ref):
     assert O.psnr(r_gpu, r_ref) >= RECON_PSNR_MIN
 
 
-GOLDEN_CASES = ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot", "kodim21_256_trained", "imagenet4_trained"]
+TRAINED_CASES = ["kodim21_256_trained", "imagenet4_trained", "kodim21_256_trained_c0.02", "imagenet4_trained_c0.02",
+                 "kodim21_256_trained_c0.03", "imagenet4_trained_c0.03"]
+GOLDEN_CASES = ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot"] + TRAINED_CASES
 
 
 @pytest.mark.parametrize("case", GOLDEN_CASES)
@@ -105,7 +108,7 @@ def test_decode_matches_golden(case, codecs, golden, manifest):
     np.testing.assert_array_equal(O.quantise_u8(rf), r)
 
 
-@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "kodim21_256_trained", "imagenet4_trained"])
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4"] + TRAINED_CASES)
 def test_end_to_end_psnr(case, codecs, golden, manifest):
     g = golden(case)
     c = codecs[manifest["cases"][case]["init"]]
@@ -251,7 +254,7 @@ def test_full_size_batch_properties(codecs, weights_spread):
                     O.decode(weights_spread, O.quantise_u8(f_ref)))
 
 
-@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "kodim21_glorot", "kodim21_256_trained", "imagenet4_trained"])
+@pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "kodim21_glorot"] + TRAINED_CASES)
 def test_entropy_matches_golden(case, codecs, golden):
     g = golden(case)
     bits, cnt = codecs["spread"].entropy(_dev(g["latent"]), counts=True)

@@ -70,11 +70,11 @@ def test_full_encoder_decoder_match_torch(golden, weights_spread):
 
 
 @pytest.mark.parametrize("case", ["kodim21_256", "imagenet4", "odd37x53", "kodim21_glorot", "kodim21_256_trained",
-                                  "imagenet4_trained"])
-def test_oracle_reproduces_golden(case, golden, manifest, weights_spread, weights_glorot, weights_trained):
+                                  "imagenet4_trained", "kodim21_256_trained_c0.02", "imagenet4_trained_c0.02",
+                                  "kodim21_256_trained_c0.03", "imagenet4_trained_c0.03"])
+def test_oracle_reproduces_golden(case, golden, manifest, weights_by_init):
     g = golden(case)
-    w = {"spread": weights_spread, "glorot": weights_glorot,
-         "trained_coef0.01": weights_trained}[manifest["cases"][case]["init"]]
+    w = weights_by_init[manifest["cases"][case]["init"]]
     f = O.encode_f32(w, g["x"])
     assert np.abs(f - g["prequant"]).max() <= 1e-6
     z = O.quantise_u8(f)
@@ -86,11 +86,11 @@ def test_oracle_reproduces_golden(case, golden, manifest, weights_spread, weight
     np.testing.assert_allclose(O.hist_entropy(g["latent"]), g["bits"], rtol=0, atol=1e-6)
 
 
-def test_weights_digest_pinned(manifest, weights_spread, weights_glorot, weights_trained):
+def test_weights_digest_pinned(manifest, weights_by_init):
     from neural_network_image_compression_amd import weights as W
-    assert W.digest(weights_spread) == manifest["weights"]["spread"]
-    assert W.digest(weights_glorot) == manifest["weights"]["glorot"]
-    assert W.digest(weights_trained) == manifest["weights"]["trained_coef0.01"]
+    assert set(weights_by_init) == set(manifest["weights"])
+    for name, w in weights_by_init.items():
+        assert W.digest(w) == manifest["weights"][name], name
 
 
 def test_colour_constants():
