@@ -57,6 +57,7 @@ struct ConvArgs {
   int ws_taps;            // weight-stationary kernels: taps per model in wx
   int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
+  int ws_xcd;             // weight-stationary kernels: logical block = XCD-contiguous remap of blockIdx
   int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment

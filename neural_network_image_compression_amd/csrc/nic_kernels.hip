@@ -2434,9 +2434,15 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
   __shared__ __attribute__((aligned(16)))
   char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 + TH * TW * COUT * 4 : 0) +
            (RESID && kResDma ? (COUT / 16) * (TH * TW / 16) * 1024 : 0)];
+  // ws_xcd: block b runs on XCD b % 8; the logical block x * (G / 8) + min(x, G % 8) + b / 8
+  // (x = b % 8, a bijection onto [0, G)) gives each XCD a contiguous range of the groups'
+  // blocks, so the tiles its blocks take at one time are neighbours whose shared halo rows /
+  // columns hit that XCD's L2
+  const int xcd = blockIdx.x & 7, ng = gridDim.x;
+  const int lb = a.ws_xcd ? xcd * (ng >> 3) + min(xcd, ng & 7) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   int gi = 0;
-  while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
-  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
+  while (gi + 1 < a.ws_ngrp && lb >= a.ws_blk[gi + 1]) ++gi;
+  const int bi = lb - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
   const int model = gi & 1;
   if constexpr (!TRP) {
     ws_body<CIN, COUT, TH, TW, RESID, 3, 3, false>(a, lds, model, bi, nb, 0, 0, 0);
@@ -5001,6 +5007,15 @@ static bool d7_grouped() {
   return on;
 }
 
+// NIC_WSX=0: weight-stationary blocks take their groups in blockIdx order (A/B of the XCD remap)
+static bool ws_xcd_remap() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_WSX");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
 // in proportion to each group's MFMA work (planes x taps).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
@@ -5034,6 +5049,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
     b = b < 1 ? 1 : b > tiles ? tiles : b;
     a.ws_blk[gi + 1] = a.ws_blk[gi] + (int)b;
   }
+  a.ws_xcd = ws_xcd_remap();
   hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP, PROJ>), dim3(a.ws_blk[a.ws_ngrp]),
                      dim3(64 * (COUT / 16)), 0, st, a);
   return hipGetLastError();
