@@ -12,11 +12,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nic.h"
@@ -1002,11 +1006,17 @@ int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pas
 // so chunk k+1's copy-in and chunk k-1's copy-out overlap chunk k's pass.  Chunk sizes ramp
 // up and down (weights min(2^i, 2^(K-1-i))): a small first chunk starts the device early and
 // a small last chunk keeps the exposed D2H tail short.
+// NIC_HOST_EDGE=e (A/B): first and last chunk e/1000 of a middle chunk, the middle ones equal.
 void host_chunk_plan(int n, int k, std::vector<int>& lo) {
+  static const int edge = [] {
+    const char* e = getenv("NIC_HOST_EDGE");
+    return e ? std::max(1, std::min(4000, atoi(e))) : 0;
+  }();
   k = std::max(1, std::min({k, n, kHostMaxChunks}));
   std::vector<double> wgt(k);
   double tot = 0;
-  for (int i = 0; i < k; ++i) tot += wgt[i] = (double)(1 << std::min(i, k - 1 - i));
+  for (int i = 0; i < k; ++i)
+    tot += wgt[i] = edge && k >= 3 ? (i == 0 || i == k - 1 ? edge / 1000.0 : 1.0) : (double)(1 << std::min(i, k - 1 - i));
   lo.assign(1, 0);
   double acc = 0;
   for (int i = 0; i < k; ++i) {
@@ -1037,6 +1047,79 @@ int grow_pinned(uint8_t*& p, size_t& have, size_t need) {
   have = need;
   return NIC_OK;
 }
+
+// Staging copies of the host-array surface (pageable <-> page-locked), split over a pool of
+// worker threads: one thread copies ~50 GB/s, so a 12.6 MB batch took 0.26 ms on the host
+// thread -- ahead of the first chunk's DMA and between the later chunks' issues, where it
+// delayed their copy-in past the previous chunk's pass.  Workers spin briefly after each copy
+// (the chunks of one call come ~0.1 ms apart), then sleep on a condition variable; the pool is
+// never destroyed (detached threads parked at exit).  NIC_HOST_COPY_THREADS: worker count
+// (default 7, plus the calling thread; 0 = plain memcpy).
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();
+    return *p;
+  }
+  void copy(void* dst, const void* src, size_t n) {
+    if (nw_ == 0 || n < kMinParallel) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    std::lock_guard<std::mutex> call(call_mu_);
+    dst_ = (char*)dst;
+    src_ = (const char*)src;
+    n_ = n;
+    pending_.store(nw_, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    part(0);
+    while (pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+  }
+
+ private:
+  static constexpr size_t kMinParallel = 256 << 10;
+  static constexpr int kSpin = 1 << 15;
+  CopyPool() {
+    const char* e = getenv("NIC_HOST_COPY_THREADS");
+    nw_ = std::max(0, std::min(31, e ? atoi(e) : 7));
+    for (int i = 0; i < nw_; ++i) std::thread([this, i] { worker(i + 1); }).detach();
+  }
+  void part(int id) {  // 4 KB-aligned share id of nw_ + 1
+    const size_t parts = (size_t)nw_ + 1, pages = (n_ + 4095) / 4096;
+    const size_t b = std::min(n_, pages * id / parts * 4096), e = std::min(n_, pages * (id + 1) / parts * 4096);
+    if (e > b) std::memcpy(dst_ + b, src_ + b, e - b);
+  }
+  void worker(int id) {
+    unsigned seen = 0;
+    for (;;) {
+      unsigned g;
+      int spins = 0;
+      while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+        if (++spins < kSpin) {
+          __builtin_ia32_pause();
+          continue;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+      }
+      seen = g;
+      part(id);
+      pending_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  int nw_ = 0;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t n_ = 0;
+  std::atomic<unsigned> gen_{0};
+  std::atomic<int> pending_{0};
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_;
+};
 
 // Host-side wait for an event: polling hipEventQuery (default) returns as soon as the GPU
 // signals, where hipEventSynchronize may sleep and pay a wake-up latency per chunk
@@ -1101,7 +1184,7 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     const size_t o0 = lo[k] * out_row, ob = (lo[k + 1] - lo[k]) * out_row;
     const uint8_t* src = in + i0;
     if (!in_pin) {
-      std::memcpy(c->pin_in + i0, in + i0, ib);
+      CopyPool::get().copy(c->pin_in + i0, in + i0, ib);
       src = c->pin_in + i0;
     }
     hipError_t e = hipMemcpyAsync(d_in + i0, src, ib, hipMemcpyHostToDevice, c->hs[0]);
@@ -1136,7 +1219,7 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
       err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
       break;
     }
-    if (!out_pin) std::memcpy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
+    if (!out_pin) CopyPool::get().copy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
   }
   for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);  // drained on every path
   if (!err && chain_check && c->range_host[4]) {
