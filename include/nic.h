@@ -13,7 +13,8 @@
  *   Decoder.__call__(z) decoder.py:39-48        nic_decode (device) / nic_decode_host (NumPy)
  *   ProClass._feed_batch pack/unpack            nic_pack_latent / nic_unpack_latent
  *     utils.py:35-36, 39-40
- *   disc_entropy tf1_13/src/training.py:66-71   nic_entropy_hist
+ *   disc_entropy tf1_13/src/training.py:66-71   nic_entropy_hist (nic_encode_entropy: fused
+ *                                                 into the encoder's conv8)
  *   tf.image.ssim_multiscale(x1, x2, 255)       nic_ms_ssim
  *     tf2_0/tests/calc_ssim.py:13
  *   PSNR (the benchmark's quality figure)       nic_sq_err
@@ -164,6 +165,15 @@ int nic_decode_host(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, 
  * bits/symbol.  Needs a ctx only for its scratch. */
 int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8, uint32_t* counts, float* bits,
                      void* stream);
+
+/* Encode + histogram entropy of the new latent in one pass (BASELINE config 5: the encoder
+ * followed by disc_entropy, tf1_13/src/training.py:66-71): same outputs as nic_encode then
+ * nic_entropy_hist -- latent, counts (nullable), bits (nullable) -- with the codes counted in
+ * conv8's epilogue as it quantises them (no re-read of the latent).  Shapes where the fold does
+ * not apply (exact-fp32 precision, latents too small for one plane per block range) run the
+ * two calls. */
+int nic_encode_entropy(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
+                       float* bits, void* stream);
 
 /* MS-SSIM of tf.image.ssim_multiscale(a, b, max_val=255) (tf2_0/tests/calc_ssim.py:13)
  * per image: a, b u8 (n,h,w,3) -> ms_ssim (n,) fp32.  TF defaults: 11-tap Gaussian

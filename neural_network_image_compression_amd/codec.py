@@ -165,6 +165,22 @@ class Codec:
         _lib.check(rc, "nic_encode")
         return (z, f) if prequant else z
 
+    def encode_entropy(self, x, counts: bool = False, out=None):
+        """encode(x) and entropy(latent) in one pass (nic_encode_entropy: the codes are counted
+        in conv8's epilogue): (latent, (3N,) fp32 bits/symbol [, (3N,256) int32 counts])."""
+        torch = _torch()
+        x = self._check_dev(x, 4, 3, "encode_entropy")
+        n, h, w, _ = x.shape
+        h8, w8 = _lib.latent_shape(h, w)
+        z = out if out is not None else torch.empty((n, h8, w8, 96), dtype=torch.uint8, device=x.device)
+        bits = torch.empty((3 * n,), dtype=torch.float32, device=x.device)
+        cnt = torch.empty((3 * n, 256), dtype=torch.int32, device=x.device) if counts else None
+        rc = self._L.nic_encode_entropy(self._h, x.data_ptr(), n, h, w, z.data_ptr(),
+                                        cnt.data_ptr() if cnt is not None else None, bits.data_ptr(),
+                                        _stream_ptr(torch, self.device))
+        _lib.check(rc, "nic_encode_entropy")
+        return (z, bits, cnt) if counts else (z, bits)
+
     def decode(self, z, rgb_f32: bool = False, out=None):
         """(N,h,w,96) u8 -> (N,8h,8w,3) u8 [, fp32 clipped RGB before quantisation]."""
         torch = _torch()

@@ -317,6 +317,9 @@ struct nic_ctx {
   size_t ws_bytes = 0;
   uint32_t* counts = nullptr;
   size_t counts_bytes = 0;
+  // set only inside nic_encode_entropy: conv8's folded-histogram partials and plane ids
+  uint32_t* fold_part = nullptr;
+  int* fold_ids = nullptr;
   char* qs = nullptr;  // MS-SSIM scratch (pooled scales + tile sums), grown on demand
   size_t qs_bytes = 0;
   // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
@@ -844,6 +847,10 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   ConvArgs a8 = conv(L_CONV8, R[3], nullptr, nullptr, h2, w2, g.c8y.out, g.c8x.out, g.c8y.lo, g.c8x.lo);
   a8.out_u8 = latent;
   a8.out_f32_latent = prequant;
+  if (x3 && c->fold_part) {  // nic_encode_entropy: the split pass's conv8 counts the codes
+    a8.hist_part = c->fold_part;
+    a8.hist_ids = c->fold_ids;
+  }
   TIMED(L_CONV8, run(L_CONV8, a8));
   if (chained) HIP_TRY(launch_fp32_chain(chain, st));
   return NIC_OK;
@@ -1211,7 +1218,8 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   // read once the streams drain: this call synchronises anyway
   const bool chain_check = !err && issued > 0 && c->precision == NIC_PRECISION_F16X3 &&
                            c->range_policy == NIC_RANGE_FALLBACK;
-  if (chain_check && hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess)
+  if (chain_check && (hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess ||
+                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess))
     err = fail(NIC_EHIP, "host surface: range-word read-back failed");
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
     hipError_t e = host_wait(c->hev[2][k]);
@@ -1221,7 +1229,15 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     }
     if (!out_pin) CopyPool::get().copy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
   }
-  for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);  // drained on every path
+  // success: every copy-in fed a pass and every pass a copy-out, so the last copy-out's event
+  // (and the read-back's) means all three streams are idle -- no stream synchronisations
+  // (~10-30 us per call); any error path drains them
+  if (!err && issued == K && chain_check) {
+    const hipError_t e = host_wait(c->hev_caller);
+    if (e != hipSuccess) err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
+  }
+  if (err || issued != K)
+    for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);
   if (!err && chain_check && c->range_host[4]) {
     HIP_TRY(hipDeviceSynchronize());
     err = chain_timeout_check(c, c->range_host, "host surface");
@@ -1320,6 +1336,57 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
     c->counts_bytes = cb;
   }
   HIP_TRY(launch_hist(latent, n, h8 * w8, c->counts, counts, bits, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+static int grow_counts(nic_ctx* c, size_t cb) {
+  if (cb <= c->counts_bytes) return NIC_OK;
+  if (c->counts) HIP_TRY(hipFree(c->counts));
+  c->counts = nullptr;
+  c->counts_bytes = 0;
+  HIP_TRY(hipMalloc(&c->counts, cb));
+  c->counts_bytes = cb;
+  return NIC_OK;
+}
+
+int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
+                       float* bits, void* stream) {
+  if (!c) return fail(NIC_EINVAL, "nic_encode_entropy: NULL ctx");
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode_entropy: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode_entropy: encoder weights not fully set");
+  if (n == 0) return NIC_OK;
+  if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode_entropy: NULL buffer");
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode_entropy: batch %d exceeds 21845 images per call", n);
+  DeviceGuard guard(c->device);
+  hipStream_t st = (hipStream_t)stream;
+  const EncGeom eg = enc_geom(n, h, w);
+  const int h8 = eg.c8y.out, w8 = eg.c8x.out;
+  if ((long long)h8 * w8 * 6 > 0x7fffffffLL) return fail(NIC_ESHAPE, "nic_encode_entropy: latent %dx%d too large", h8, w8);
+  const bool fits = x3_plane_fits(eg.c2y.out, eg.c2x.out);
+  // the fold needs the split-f16 pass with the tap-split conv8 and block ranges within a plane;
+  // otherwise (and for counts == bits == NULL) the two-step form
+  const bool fold = (counts || bits) && c->precision == NIC_PRECISION_F16X3 && fits && conv12_fused() &&
+                    hist_fold_supported(n, h8, w8);
+  if (!fold) {
+    int rc = nic_encode(c, rgb, n, h, w, latent, nullptr, stream);
+    if (rc || (!counts && !bits)) return rc;
+    return nic_entropy_hist(c, latent, n, h8, w8, counts, bits, stream);
+  }
+  int rc = grow_counts(c, hist_fold_scratch_bytes(n, h8, w8));
+  if (rc) return rc;
+  const size_t fb = hist_fold_scratch_bytes(n, h8, w8);
+  c->fold_part = c->counts;
+  c->fold_ids = (int*)((char*)c->counts + fb / (512 * sizeof(uint32_t) + 2 * sizeof(int)) * 512 * sizeof(uint32_t));
+  rc = guarded(c, st, "nic_encode_entropy", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
+    return encode_pass(c, rgb, n, h, w, latent, nullptr, st, x3, rg, timed);
+  });
+  c->fold_part = nullptr;
+  c->fold_ids = nullptr;
+  if (rc) return rc;
+  RangeGuard trip{};  // the split pass's epoch: a trip means the re-run rewrote the latent
+  trip.flag = c->range;
+  trip.epoch = c->epoch;
+  HIP_TRY(launch_hist_fold(c->counts, latent, n, h8, w8, trip, counts, bits, st));
   return NIC_OK;
 }
 

@@ -59,6 +59,10 @@ struct ConvArgs {
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
   int ws_xcd;             // weight-stationary kernels: logical block = XCD-contiguous remap of blockIdx
   int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
+  // conv8 (f16x3, OUT_U8_LATENT) with the latent histogram folded into its epilogue
+  // (nic_encode_entropy): per block [2 planes][256] partial counts and the 2 plane ids
+  uint32_t* hist_part;
+  int* hist_ids;
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
   const uint16_t* wx2;
@@ -166,6 +170,14 @@ hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st);
 size_t hist_scratch_bytes(int nimg, int plane_px);
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
                        hipStream_t st);
+// the histogram folded into conv8 (nic_encode_entropy): whether the split-f16 conv8 launch can
+// count for this shape (each block's contiguous tile range spans at most two planes), the
+// partial-count scratch it needs (ids follow the counts), and the reduce (counts / bits; a
+// tripped range guard -- the latent rewritten by the exact-fp32 re-run -- recounts from z)
+bool hist_fold_supported(int nimg, int h8, int w8);
+size_t hist_fold_scratch_bytes(int nimg, int h8, int w8);
+hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
+                            uint32_t* counts, float* bits, hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 
 // --- quality metrics (nic_quality.hip) ---------------------------------------------------

@@ -1660,9 +1660,17 @@ constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
 // the last column read a finite 0 for the zero weight of kw = 5
 constexpr int C12_PP = 52;
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1>
+// HIST (conv8 in nic_encode_entropy): each block takes a contiguous range of its group's
+// tiles (at most two planes, hist_fold_supported) instead of every nb-th tile, and the ts = 0
+// epilogue counts the u8 codes into per-block LDS histograms [2 planes][256][HR replicas]
+// (code 0 counted per lane in a register: trained latents are mostly zeros), written out as
+// partial counts at the end (hist_fold_kernel reduces them).
+constexpr int HIST_R = 4;
+constexpr int HIST_LDS = 2 * 256 * HIST_R * 4;
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1, bool HIST = false>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
+  static_assert(!HIST || (OUT_MODE == OUT_U8_LATENT && !FUSE1), "histogram fold: conv8 only");
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
   static_assert(!FUSE1 || (CIN == 32 && TH == 8 && G::HH == 19 && NTS == 2 && OUT_MODE == OUT_SPLIT),
@@ -1680,7 +1688,17 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int per_plane = a.tiles_y * a.tiles_x;
   const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
-  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  int walk_b = bi, walk_n = nb, hplane0 = 0;  // tile walk: start, stride; HIST: first plane
+  if constexpr (HIST) {
+    const long long t0 = (long long)bi * ntot / nb, t1 = (long long)(bi + 1) * ntot / nb;
+    walk_b = (int)t0;
+    walk_n = 1;
+    ntile = (int)(t1 - t0);
+    hplane0 = p0 + (int)(t0 / per_plane);
+  }
+  uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [2][256][HIST_R]
+  uint32_t hz0 = 0, hz1 = 0;  // HIST: this lane's code-0 counts of the block's two planes
 
   f16x8 wr[NT][KST][2];
   {
@@ -1704,8 +1722,10 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
   // tiles walked in order by each call sequence (DMA issue, epilogue, FUSE1 RGB loads)
   TileWalk w_issue, w_ep, w_rgb;
-  w_issue.init(bi, nb, a.tiles_y, a.tiles_x);
+  w_issue.init(walk_b, walk_n, a.tiles_y, a.tiles_x);
   w_ep = w_rgb = w_issue;
+  if constexpr (HIST)
+    for (int q = threadIdx.x; q < 2 * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
   auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
     int pl, ty, tx;
     w.take(pl, ty, tx);
@@ -1860,6 +1880,20 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
               }
               *(uint32_t*)(a.out_u8 + lo) = packed;
               if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
+              if constexpr (HIST) {
+                const bool second = ep_p != hplane0;  // wave-uniform
+                uint32_t* hs = hist + (second ? 256 * HIST_R : 0) + (lane & (HIST_R - 1));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const uint32_t code = (packed >> (8 * r)) & 255;
+                  if (code == 0) {
+                    hz0 += second ? 0u : 1u;
+                    hz1 += second ? 1u : 0u;
+                  } else {
+                    atomicAdd(hs + code * HIST_R, 1u);
+                  }
+                }
+              }
             }
           }
         }
@@ -1993,6 +2027,27 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
   }
   range_report(a.rg, rmax);
+  if constexpr (HIST) {  // code-0 counts into bin 0, then the block's partial counts and plane ids
+    for (int o = 32; o > 0; o >>= 1) {
+      hz0 += __shfl_xor(hz0, o);
+      hz1 += __shfl_xor(hz1, o);
+    }
+    if (TS == 0 && lane == 0) {
+      if (hz0) atomicAdd(hist, hz0);
+      if (hz1) atomicAdd(hist + 256 * HIST_R, hz1);
+    }
+    __syncthreads();
+    const int slot = a.ws_blk[model] + bi;  // logical block: ranges in order within the group
+    const int q = threadIdx.x;              // 512 threads = 2 planes x 256 bins
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < HIST_R; ++r) c += hist[q * HIST_R + r];
+    a.hist_part[(size_t)slot * 512 + q] = c;
+    if (q < 2) {
+      const int last = ntile > 0 ? p0 + (int)(((long long)walk_b + ntile - 1) / per_plane) : -1;
+      a.hist_ids[slot * 2 + q] = ntile == 0 ? -1 : q == 0 ? hplane0 : (last > hplane0 ? hplane0 + 1 : -1);
+    }
+  }
 #ifdef NIC_STAMPS
   if (lane == 0) {
     unsigned long long* o = g_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
@@ -2407,14 +2462,15 @@ __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
     c12_wave<1>(a, lds, gi, bi, nb);
 }
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1, bool HIST = false>
 __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
   using G = GeomS2<CIN, TH, 8>;
   constexpr int NCG = COUT / 16;
   static_assert(NCG * NTS == 8, "8 waves per block");
   constexpr int PARTS = 2 * (NTS - 1) * NCG * (TH / 2) * 1024;
   __shared__ __attribute__((aligned(16)))
-  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PP + 256) * 4 : 0)];
+  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PP + 256) * 4 : 0) +
+           (HIST ? HIST_LDS : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -2422,7 +2478,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
-    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS, FUSE1>(a, lds, gi, bi, nb);
+    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS, FUSE1, HIST>(a, lds, gi, bi, nb);
   });
 }
 
@@ -4609,12 +4665,30 @@ __global__ __launch_bounds__(NT) void latent_hist_kernel(const uint8_t* __restri
   }
 }
 
+// Plane p's entropy from its 256 counts (thread `bin` < 256 holds count c; threads 0-255 are
+// waves 0-3): p_i = c_i / N (fp32), term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2), summed in
+// double in a fixed order (64-lane butterflies, then the 4 waves) -- shared by both reduces so
+// their bits agree exactly.  Ends with a block barrier; thread 0 writes bits[p].
+__device__ __forceinline__ void plane_entropy(uint32_t c, int bin, int p, float n_sym, uint32_t* __restrict__ counts,
+                                              float* __restrict__ bits, double* red) {
+  double s = 0.0;
+  if (bin < 256) {
+    if (counts) counts[(size_t)p * 256 + bin] = c;
+    const float pr = __fdiv_rn((float)c, n_sym);
+    const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
+    s = (double)__fmul_rn(pr, __fdiv_rn(-lg, 0.693147182464599609375f));
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((bin & 63) == 0) red[bin >> 6] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && bits) bits[p] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+}
+
 __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __restrict__ part, int chunks, float n_sym,
                                                             uint32_t* __restrict__ counts, float* __restrict__ bits) {
   // one block per plane p; thread (g, q) sums bins 4q..4q+3 (one 16-B load) of every 16th
   // partial of the plane (exact integers, 16 loads in flight: one round covers 256 partials),
-  // the 16 groups meet in LDS.  Then p_i = c_i / N (fp32),
-  // term = p_i * (-log(clip(p_i, 1e-5, 1)) / log 2), summed in double.
+  // the 16 groups meet in LDS; then plane_entropy
   __shared__ u32x4 grp[16][64];
   __shared__ double red[4];
   const int p = blockIdx.x;
@@ -4636,17 +4710,47 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
 #pragma unroll
     for (int j = 0; j < 16; ++j) c += ((const uint32_t*)grp[j])[bin];
   }
-  double s = 0.0;
-  if (bin < 256) {
-    if (counts) counts[(size_t)p * 256 + bin] = c;
-    const float pr = __fdiv_rn((float)c, n_sym);
-    const float lg = logf(fminf(fmaxf(pr, 1e-5f), 1.0f));
-    s = (double)__fmul_rn(pr, __fdiv_rn(-lg, 0.693147182464599609375f));
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if ((bin & 63) == 0) red[bin >> 6] = s;
+  plane_entropy(c, bin, p, n_sym, counts, bits, red);
+}
+
+// The folded histogram's reduce (nic_encode_entropy): plane p sums the partial counts of the
+// conv8 blocks whose tile ranges meet it (plane ids stored beside the counts; the candidate
+// blocks follow from the contiguous ranges).  If the split pass tripped the range guard, the
+// latent was rewritten by the exact-fp32 re-run after conv8 counted: the plane is recounted
+// from z (LDS atomics; the rare path).
+__global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restrict__ part, const int* __restrict__ ids,
+                                                        int nimg, int per_plane, int by, int bc,
+                                                        const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
+                                                        float n_sym, uint32_t* __restrict__ counts,
+                                                        float* __restrict__ bits) {
+  __shared__ uint32_t h[256];
+  __shared__ double red[4];
+  const int p = blockIdx.x, bin = threadIdx.x;
+  const bool tripped = trip.flag && *(volatile const int*)trip.flag == trip.epoch;
+  uint32_t c = 0;
+  if (!tripped) {
+    const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0;
+    const long long ntot = (long long)(gi ? 2 * nimg : nimg) * per_plane, pl = p - (gi ? nimg : 0);
+    const int b0 = (int)std::max(0LL, pl * per_plane * nb / ntot - 1);
+    const int b1 = (int)std::min((long long)nb - 1, ((pl + 1) * per_plane * nb + ntot - 1) / ntot + 1);
+    for (int b = b0; b <= b1; ++b)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        if (ids[(base + b) * 2 + s] == p) c += part[((size_t)(base + b) * 2 + s) * 256 + bin];
+  } else {
+    h[bin] = 0;
+    __syncthreads();
+    const int n = p % nimg, type = p / nimg;
+    const uint8_t* src = z + (size_t)n * plane_px * 96 + type * 32;
+    for (long long i = bin; i < (long long)plane_px * 8; i += 256) {
+      const uint32_t w = *(const uint32_t*)(src + (i >> 3) * 96 + (i & 7) * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(&h[(w >> (8 * k)) & 255], 1u);
+    }
+    __syncthreads();
+    c = h[bin];
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && bits) bits[p] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+  plane_entropy(c, bin, p, n_sym, counts, bits, red);
 }
 
 __global__ __launch_bounds__(256) void pack_latent_kernel(const uint8_t* __restrict__ z, uint8_t* __restrict__ out,
@@ -5131,6 +5235,31 @@ static bool ws2_tile_xcd() {
 
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
 // proportion to their planes.
+static void ws2_groups(int nimg, long long per_plane, int* by, int* bc) {
+  const int target = device_cus();
+  const long long ty = per_plane * nimg, tc = per_plane * 2 * nimg;
+  long long y = std::max(1LL, std::min((long long)(target + 1) / 3, ty));
+  *by = (int)y;
+  *bc = (int)std::max(1LL, std::min((long long)target - y, tc));
+}
+
+// conv8's tile grid (4 x 8 output tiles) and the fold's condition: every block's contiguous
+// range (ceil(tiles / blocks) of its group) fits in one plane's tiles, so it meets <= 2 planes
+bool hist_fold_supported(int nimg, int h8, int w8) {
+  if (nimg <= 0 || h8 <= 0 || w8 <= 0) return false;
+  const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
+  int by, bc;
+  ws2_groups(nimg, pp, &by, &bc);
+  return (pp * nimg + by - 1) / by <= pp && (pp * 2 * nimg + bc - 1) / bc <= pp;
+}
+
+size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {
+  const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
+  int by, bc;
+  ws2_groups(nimg, pp, &by, &bc);
+  return (size_t)(by + bc) * (512 * sizeof(uint32_t) + 2 * sizeof(int));
+}
+
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
 static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.tiles_y = (a.OH + TH - 1) / TH;
@@ -5142,19 +5271,25 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ntiles = (int)nt;
   a.ws_taps = 25;
   a.ws_ngrp = 2;
-  const int target = device_cus();
-  const long long ty = per_plane * a.nimg, tc = per_plane * (a.P - a.nimg);
-  long long by = (target + 1) / 3;
-  by = std::max(1LL, std::min(by, ty));
-  long long bc = std::max(1LL, std::min((long long)target - by, tc));
+  int by, bc;
+  ws2_groups(a.nimg, per_plane, &by, &bc);
   a.ws_blk[0] = 0;
-  a.ws_blk[1] = (int)by;
-  a.ws_blk[2] = (int)(by + bc);
+  a.ws_blk[1] = by;
+  a.ws_blk[2] = by + bc;
   a.tile_xcd = ws2_tile_xcd() ? 1 : 0;
-  if constexpr (PIPE12)
+  if constexpr (PIPE12) {
     hipLaunchKernelGGL(conv12_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
-  else
+  } else if constexpr (OUT_MODE == OUT_U8_LATENT && !FUSE1) {
+    if (a.hist_part) {
+      if (!a.hist_ids || !hist_fold_supported(a.nimg, a.OH, a.OW)) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1, true>), dim3(a.ws_blk[2]), dim3(512), 0,
+                         st, a);
+    } else {
+      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+    }
+  } else {
     hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -5435,6 +5570,18 @@ hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part,
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, chunks, (float)plane_px * 32.0f,
                      counts, bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
+                            uint32_t* counts, float* bits, hipStream_t st) {
+  if (!hist_fold_supported(nimg, h8, w8)) return hipErrorInvalidValue;
+  const int pp = ((h8 + 3) / 4) * ((w8 + 7) / 8);
+  int by, bc;
+  ws2_groups(nimg, pp, &by, &bc);
+  const int* ids = (const int*)(part + (size_t)(by + bc) * 512);
+  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, ids, nimg, pp, by, bc, z, h8 * w8, trip,
+                     (float)h8 * w8 * 32.0f, counts, bits);
   return hipGetLastError();
 }
 

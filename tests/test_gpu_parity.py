@@ -262,6 +262,49 @@ def test_entropy_matches_golden(case, codecs, golden):
     np.testing.assert_allclose(bits.cpu().numpy(), g["bits"].ravel(), rtol=0, atol=2e-6)
 
 
+@pytest.mark.parametrize("shape", [(64, 256, 256), (2, 2160, 3840), (4, 128, 128), (3, 37, 53), (1, 8, 8),
+                                   (2, 1, 2400), (1000, 8, 8)],
+                         ids=["config2", "4k", "imagenet", "odd", "tiny", "one-row", "many-tiny-unfolded"])
+def test_encode_entropy_fold(shape, weights_spread, weights_trained):
+    """nic_encode_entropy (the latent histogram counted in conv8's epilogue, BASELINE config 5)
+    against nic_encode + nic_entropy_hist: latent, counts and bits bit-exact, with seeded and
+    trained (zero-heavy latents) weights; shapes whose block ranges would span more than two
+    planes take the two-call path (tiny-unfolded); counts also equal the oracle's."""
+    from neural_network_image_compression_amd.codec import Codec
+    n, h, w = shape
+    x = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(n * h + w))
+    xd = x.cuda()
+    for wts in (weights_spread, weights_trained):
+        c = Codec(0)
+        c.set_weights(wts)
+        z1, bits1, cnt1 = c.encode_entropy(xd, counts=True)
+        z2 = c.encode(xd)
+        bits2, cnt2 = c.entropy(z2, counts=True)
+        assert torch.equal(z1, z2)
+        assert torch.equal(cnt1, cnt2)
+        assert torch.equal(bits1, bits2)
+        if n * h * w <= 64 * 256 * 256:
+            np.testing.assert_array_equal(cnt1.cpu().numpy(), O.histograms(z1.cpu().numpy()))
+        zb, bb = c.encode_entropy(xd)  # counts not requested
+        assert torch.equal(zb, z1) and torch.equal(bb, bits1)
+        del z1, z2, zb
+
+
+def test_encode_entropy_fold_after_range_trip(golden, weights_spread):
+    """A tripped split pass: the exact-fp32 re-run rewrites the latent after conv8 counted, so
+    the fold's reduce recounts from the new latent -- counts / bits equal the two-call form."""
+    from neural_network_image_compression_amd.codec import Codec
+    g = golden("kodim21_256")
+    c = Codec(0)
+    c.set_weights(range_scaled_weights(weights_spread))
+    x = _dev(np.concatenate([g["x"]] * 4))
+    z1, bits1, cnt1 = c.encode_entropy(x, counts=True)
+    assert c.range_trips() == 1
+    bits2, cnt2 = c.entropy(z1, counts=True)
+    assert torch.equal(cnt1, cnt2) and torch.equal(bits1, bits2)
+    check_codes(z1[:1].cpu().numpy(), g["latent"], g["prequant"])
+
+
 def test_entropy_large_and_edge_planes(codecs):
     rng = np.random.default_rng(5)
     z = rng.integers(0, 256, (1, 270, 480, 96), dtype=np.uint8)  # one 4K frame's latent

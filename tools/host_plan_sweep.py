@@ -1,7 +1,7 @@
 """Host-array surface (Encoder()(numpy) -> Decoder()(numpy), config-2 batch) per chunk plan and
 staging-copy thread count, each setting in a fresh process (the switches are read at library
 load): NIC_HOST_EDGE (edge-chunk weight, permille of a middle chunk), chunks, and
-NIC_HOST_COPY_THREADS.  Prints one JSON line per setting; usage: python tools/host_plan_sweep.py"""
+NIC_HOST_COPY_THREADS.  Prints one JSON line per setting; usage: python tools/host_plan_sweep.py [n settings]"""
 import json
 import os
 import subprocess
@@ -38,7 +38,7 @@ SETTINGS = [("3", {}), ("3", {"NIC_HOST_COPY_THREADS": "0"}), ("3", {"NIC_HOST_E
             ("3", {"NIC_HOST_EDGE": "350"}), ("4", {"NIC_HOST_EDGE": "300"}), ("4", {}), ("2", {}),
             ("5", {"NIC_HOST_EDGE": "300"})]
 
-for chunks, env in SETTINGS:
+for chunks, env in SETTINGS[:int(sys.argv[1]) if len(sys.argv) > 1 else None]:
     e = dict(os.environ, **env)
     out = subprocess.run([sys.executable, "-c", CHILD, chunks], env=e, capture_output=True, text=True, timeout=240)
     line = out.stdout.strip().splitlines()[-1] if out.returncode == 0 and out.stdout.strip() else None

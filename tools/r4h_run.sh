@@ -1,0 +1,23 @@
+#!/bin/bash
+# round 4: histogram fold (tests + 4K A/B), conv8 stamps
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
+  -k "encode_entropy or entropy or range_guard" > gpurun_out/r4h_tests.log 2>&1; rc=$?
+echo "[tests] rc=$rc"; tail -4 gpurun_out/r4h_tests.log
+[ $rc -eq 0 ] || exit $rc
+B="--workload 4k --steps 10 --warmup 3 --no-cpu-baseline --no-parity --no-power-probe --no-host-path --no-quality"
+for r in 1 2; do
+  timeout -k 10 300 python bench.py $B > gpurun_out/r4h_4k_fold_$r.json 2> gpurun_out/r4h_4k_fold_$r.err || { echo "fold $r failed"; tail -3 gpurun_out/r4h_4k_fold_$r.err; exit 1; }
+  NIC_BENCH_HIST=sep timeout -k 10 300 python bench.py $B > gpurun_out/r4h_4k_sep_$r.json 2> gpurun_out/r4h_4k_sep_$r.err || { echo "sep $r failed"; exit 1; }
+done
+python3 - <<'PY'
+import json
+for t in ("fold_1","sep_1","fold_2","sep_2"):
+    d=json.loads(open(f"gpurun_out/r4h_4k_{t}.json").read().strip().splitlines()[-1])
+    print(t, d["value"], d["ms_per_step"], {k: v.get("avg_ms") for k, v in d["layers"].items()})
+PY
+timeout -k 10 120 ./ab/c8_stamps > gpurun_out/r4h_c8_stamps.txt 2>&1; echo "[c8] rc=$?"; cat gpurun_out/r4h_c8_stamps.txt
+timeout -k 10 200 python tools/host_plan_sweep.py 2 > gpurun_out/r4h_host.jsonl 2>&1; echo "[host] rc=$?"; cat gpurun_out/r4h_host.jsonl
