@@ -1374,9 +1374,10 @@ int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint
   }
   int rc = grow_counts(c, hist_fold_scratch_bytes(n, h8, w8));
   if (rc) return rc;
+  // counts [blocks][slots][256], then ids [blocks][slots] (hist_fold_scratch_bytes)
   const size_t fb = hist_fold_scratch_bytes(n, h8, w8);
   c->fold_part = c->counts;
-  c->fold_ids = (int*)((char*)c->counts + fb / (512 * sizeof(uint32_t) + 2 * sizeof(int)) * 512 * sizeof(uint32_t));
+  c->fold_ids = (int*)((char*)c->counts + fb / (256 * sizeof(uint32_t) + sizeof(int)) * 256 * sizeof(uint32_t));
   rc = guarded(c, st, "nic_encode_entropy", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
     return encode_pass(c, rgb, n, h, w, latent, nullptr, st, x3, rg, timed);
   });

@@ -1660,13 +1660,26 @@ constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
 // the last column read a finite 0 for the zero weight of kw = 5
 constexpr int C12_PP = 52;
 
-// HIST (conv8 in nic_encode_entropy): each block takes a contiguous range of its group's
-// tiles (at most two planes, hist_fold_supported) instead of every nb-th tile, and the ts = 0
-// epilogue counts the u8 codes into per-block LDS histograms [2 planes][256][HR replicas]
-// (code 0 counted per lane in a register: trained latents are mostly zeros), written out as
-// partial counts at the end (hist_fold_kernel reduces them).
-constexpr int HIST_R = 4;
-constexpr int HIST_LDS = 2 * 256 * HIST_R * 4;
+// HIST (conv8 in nic_encode_entropy): the ts = 0 epilogue also counts the u8 codes into
+// per-block LDS histograms [HIST_S planes][256][HIST_R replicas] (code 0 counted per lane in
+// registers: trained latents are mostly zeros), written out as partial counts + plane ids at
+// the end (hist_fold_kernel reduces them).  So that a block meets at most HIST_S planes, the
+// group's tiles are cut into one contiguous range per XCD (in proportion to its blocks) and
+// the XCD's blocks stride through their range -- at each step an XCD still works on a
+// contiguous strip of tiles (shared halo rows / columns in its L2), as the default walk does.
+// (A contiguous range per block, ~two planes: conv8 0.891 -> 1.069 ms on 4K frames, the halo
+// sharing between concurrently running neighbour tiles lost.)
+constexpr int HIST_R = 2, HIST_S = 4;
+constexpr int HIST_LDS = HIST_S * 256 * HIST_R * 4;
+__host__ __device__ inline void hist_xcd_range(int rel, int nb, long long ntot, long long* start, long long* len, int* nx,
+                                               int* j) {
+  const int x = rel & 7, q = nb >> 3, r = nb & 7;
+  const int px = x * q + (x < r ? x : r);  // first position of XCD class x (xcd_pos)
+  *nx = q + (x < r ? 1 : 0);
+  *j = rel >> 3;
+  *start = (long long)px * ntot / nb;
+  *len = (long long)(px + *nx) * ntot / nb - *start;
+}
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1, bool HIST = false>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
@@ -1690,15 +1703,17 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int ntot = np * per_plane;
   int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
   int walk_b = bi, walk_n = nb, hplane0 = 0;  // tile walk: start, stride; HIST: first plane
-  if constexpr (HIST) {
-    const long long t0 = (long long)bi * ntot / nb, t1 = (long long)(bi + 1) * ntot / nb;
-    walk_b = (int)t0;
-    walk_n = 1;
-    ntile = (int)(t1 - t0);
-    hplane0 = p0 + (int)(t0 / per_plane);
+  if constexpr (HIST) {  // bi = the block's group-relative index (not xcd_pos): its XCD range
+    long long st, len;
+    int nx, j;
+    hist_xcd_range(bi, nb, ntot, &st, &len, &nx, &j);
+    walk_b = (int)(st + j);
+    walk_n = nx;
+    ntile = j < len ? (int)((len - j + nx - 1) / nx) : 0;
+    hplane0 = p0 + (int)((st + j) / per_plane);
   }
-  uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [2][256][HIST_R]
-  uint32_t hz0 = 0, hz1 = 0;  // HIST: this lane's code-0 counts of the block's two planes
+  uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [HIST_S][256][HIST_R]
+  uint32_t hz[HIST_S] = {};  // HIST: this lane's code-0 counts per plane slot
 
   f16x8 wr[NT][KST][2];
   {
@@ -1725,7 +1740,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   w_issue.init(walk_b, walk_n, a.tiles_y, a.tiles_x);
   w_ep = w_rgb = w_issue;
   if constexpr (HIST)
-    for (int q = threadIdx.x; q < 2 * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
+    for (int q = threadIdx.x; q < HIST_S * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
   auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
     int pl, ty, tx;
     w.take(pl, ty, tx);
@@ -1881,18 +1896,20 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
               *(uint32_t*)(a.out_u8 + lo) = packed;
               if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
               if constexpr (HIST) {
-                const bool second = ep_p != hplane0;  // wave-uniform
-                uint32_t* hs = hist + (second ? 256 * HIST_R : 0) + (lane & (HIST_R - 1));
+                const int slot = ep_p - hplane0;  // wave-uniform, < HIST_S (hist_fold_supported)
+                uint32_t* hs = hist + slot * (256 * HIST_R) + (lane & (HIST_R - 1));
+                uint32_t zc = 0;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const uint32_t code = (packed >> (8 * r)) & 255;
-                  if (code == 0) {
-                    hz0 += second ? 0u : 1u;
-                    hz1 += second ? 1u : 0u;
-                  } else {
+                  if (code == 0)
+                    ++zc;
+                  else
                     atomicAdd(hs + code * HIST_R, 1u);
-                  }
                 }
+                static_for<HIST_S>([&](auto k) {  // registers, not a scratch-indexed array
+                  if (slot == decltype(k)::value) hz[decltype(k)::value] += zc;
+                });
               }
             }
           }
@@ -2028,24 +2045,24 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   }
   range_report(a.rg, rmax);
   if constexpr (HIST) {  // code-0 counts into bin 0, then the block's partial counts and plane ids
-    for (int o = 32; o > 0; o >>= 1) {
-      hz0 += __shfl_xor(hz0, o);
-      hz1 += __shfl_xor(hz1, o);
-    }
-    if (TS == 0 && lane == 0) {
-      if (hz0) atomicAdd(hist, hz0);
-      if (hz1) atomicAdd(hist + 256 * HIST_R, hz1);
-    }
+    static_for<HIST_S>([&](auto k) {
+      constexpr int K = decltype(k)::value;
+      uint32_t z = hz[K];
+      for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
+      if (TS == 0 && lane == 0 && z) atomicAdd(hist + K * 256 * HIST_R, z);
+    });
     __syncthreads();
-    const int slot = a.ws_blk[model] + bi;  // logical block: ranges in order within the group
-    const int q = threadIdx.x;              // 512 threads = 2 planes x 256 bins
-    uint32_t c = 0;
+    const int blk = a.ws_blk[model] + bi;  // the launch's block slot of the partials
+    for (int q = threadIdx.x; q < HIST_S * 256; q += 64 * NW) {
+      uint32_t c = 0;
 #pragma unroll
-    for (int r = 0; r < HIST_R; ++r) c += hist[q * HIST_R + r];
-    a.hist_part[(size_t)slot * 512 + q] = c;
-    if (q < 2) {
-      const int last = ntile > 0 ? p0 + (int)(((long long)walk_b + ntile - 1) / per_plane) : -1;
-      a.hist_ids[slot * 2 + q] = ntile == 0 ? -1 : q == 0 ? hplane0 : (last > hplane0 ? hplane0 + 1 : -1);
+      for (int r = 0; r < HIST_R; ++r) c += hist[q * HIST_R + r];
+      a.hist_part[(size_t)blk * HIST_S * 256 + q] = c;
+    }
+    if (threadIdx.x < HIST_S) {
+      const int last = ntile > 0 ? p0 + (int)(((long long)walk_b + (long long)(ntile - 1) * walk_n) / per_plane) : -1;
+      const int pid = hplane0 + (int)threadIdx.x;
+      a.hist_ids[blk * HIST_S + threadIdx.x] = ntile > 0 && pid <= last ? pid : -1;
     }
   }
 #ifdef NIC_STAMPS
@@ -2474,7 +2491,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  const int bi = a.tile_xcd ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
+  const int bi = a.tile_xcd && !HIST ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
@@ -4728,15 +4745,12 @@ __global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restri
   const int p = blockIdx.x, bin = threadIdx.x;
   const bool tripped = trip.flag && *(volatile const int*)trip.flag == trip.epoch;
   uint32_t c = 0;
-  if (!tripped) {
+  if (!tripped) {  // every block of the plane's group, every slot whose id is p (fixed order)
     const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0;
-    const long long ntot = (long long)(gi ? 2 * nimg : nimg) * per_plane, pl = p - (gi ? nimg : 0);
-    const int b0 = (int)std::max(0LL, pl * per_plane * nb / ntot - 1);
-    const int b1 = (int)std::min((long long)nb - 1, ((pl + 1) * per_plane * nb + ntot - 1) / ntot + 1);
-    for (int b = b0; b <= b1; ++b)
+    for (int b = base; b < base + nb; ++b)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        if (ids[(base + b) * 2 + s] == p) c += part[((size_t)(base + b) * 2 + s) * 256 + bin];
+      for (int s = 0; s < HIST_S; ++s)
+        if (ids[b * HIST_S + s] == p) c += part[((size_t)b * HIST_S + s) * 256 + bin];
   } else {
     h[bin] = 0;
     __syncthreads();
@@ -5243,21 +5257,32 @@ static void ws2_groups(int nimg, long long per_plane, int* by, int* bc) {
   *bc = (int)std::max(1LL, std::min((long long)target - y, tc));
 }
 
-// conv8's tile grid (4 x 8 output tiles) and the fold's condition: every block's contiguous
-// range (ceil(tiles / blocks) of its group) fits in one plane's tiles, so it meets <= 2 planes
+// conv8's tile grid (4 x 8 output tiles) and the fold's condition: every XCD range of tiles
+// (hist_xcd_range) spans at most HIST_S planes -- large frames (config 5: 2 XCD ranges per
+// 4K plane); batches of small images run the two-call form
 bool hist_fold_supported(int nimg, int h8, int w8) {
   if (nimg <= 0 || h8 <= 0 || w8 <= 0) return false;
   const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  return (pp * nimg + by - 1) / by <= pp && (pp * 2 * nimg + bc - 1) / bc <= pp;
+  for (int gi = 0; gi < 2; ++gi) {
+    const int nb = gi ? bc : by;
+    const long long ntot = pp * (gi ? 2 : 1) * nimg;
+    for (int x = 0; x < 8 && x < nb; ++x) {
+      long long st, len;
+      int nx, j;
+      hist_xcd_range(x, nb, ntot, &st, &len, &nx, &j);
+      if (len > 0 && (st + len - 1) / pp - st / pp + 1 > HIST_S) return false;
+    }
+  }
+  return true;
 }
 
 size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {
   const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  return (size_t)(by + bc) * (512 * sizeof(uint32_t) + 2 * sizeof(int));
+  return (size_t)(by + bc) * HIST_S * (256 * sizeof(uint32_t) + sizeof(int));
 }
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
@@ -5579,7 +5604,7 @@ hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, in
   const int pp = ((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  const int* ids = (const int*)(part + (size_t)(by + bc) * 512);
+  const int* ids = (const int*)(part + (size_t)(by + bc) * HIST_S * 256);
   hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, ids, nimg, pp, by, bc, z, h8 * w8, trip,
                      (float)h8 * w8 * 32.0f, counts, bits);
   return hipGetLastError();
