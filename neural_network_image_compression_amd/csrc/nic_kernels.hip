@@ -1670,7 +1670,11 @@ constexpr int C12_PP = 52;
 // (A contiguous range per block, ~two planes: conv8 0.891 -> 1.069 ms on 4K frames, the halo
 // sharing between concurrently running neighbour tiles lost.)
 constexpr int HIST_R = 2, HIST_S = 4;
-constexpr int HIST_LDS = HIST_S * 256 * HIST_R * 4;
+// + the codes of the last two tiles ([2 parities][NCG][MT][64 lanes] u32, conv8: 2 KB): the
+// ts = 0 epilogue stores them, the ts = 1 waves (which wait ~1,700 cycles per tile at the top
+// barrier, tools/c8_stamps.cpp) count them one tile later -- counting in the ts = 0 epilogue
+// itself lengthened the critical pair of waves (conv8 +12 % on 4K frames)
+constexpr int HIST_LDS = HIST_S * 256 * HIST_R * 4 + 2 * 2 * 2 * 64 * 4;
 __host__ __device__ inline void hist_xcd_range(int rel, int nb, long long ntot, long long* start, long long* len, int* nx,
                                                int* j) {
   const int x = rel & 7, q = nb >> 3, r = nb & 7;
@@ -1713,7 +1717,33 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     hplane0 = p0 + (int)((st + j) / per_plane);
   }
   uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [HIST_S][256][HIST_R]
+  uint32_t* codes = hist + HIST_S * 256 * HIST_R;                    // HIST: [2][NCG][MT][64]
   uint32_t hz[HIST_S] = {};  // HIST: this lane's code-0 counts per plane slot
+  int hq_p = 0, hq_y = 0, hq_x = 0;  // HIST: the tile whose codes the ts = 1 waves count next
+  // HIST, ts = 1: count the codes the ts = 0 wave of this cg stored for tile (p, y, x)
+  auto hist_count = [&](int p, int ty0, int tx0, int par) __attribute__((always_inline)) {
+    const int slot = p - hplane0;  // wave-uniform, < HIST_S (hist_fold_supported)
+    uint32_t* hs = hist + slot * (256 * HIST_R) + (lane & (HIST_R - 1));
+    uint32_t zc = 0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int oy = ty0 + 2 * m + (l16 >> 3), ox = tx0 + (l16 & 7);
+      if (oy < a.OH && ox < a.OW) {
+        const uint32_t w = codes[((par * NCG + cg) * MT + m) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t code = (w >> (8 * r)) & 255;
+          if (code == 0)
+            ++zc;
+          else
+            atomicAdd(hs + code * HIST_R, 1u);
+        }
+      }
+    }
+    static_for<HIST_S>([&](auto k) {  // registers, not a scratch-indexed array
+      if (slot == decltype(k)::value) hz[decltype(k)::value] += zc;
+    });
+  };
 
   f16x8 wr[NT][KST][2];
   {
@@ -1895,30 +1925,22 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
               }
               *(uint32_t*)(a.out_u8 + lo) = packed;
               if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v;
-              if constexpr (HIST) {
-                const int slot = ep_p - hplane0;  // wave-uniform, < HIST_S (hist_fold_supported)
-                uint32_t* hs = hist + slot * (256 * HIST_R) + (lane & (HIST_R - 1));
-                uint32_t zc = 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const uint32_t code = (packed >> (8 * r)) & 255;
-                  if (code == 0)
-                    ++zc;
-                  else
-                    atomicAdd(hs + code * HIST_R, 1u);
-                }
-                static_for<HIST_S>([&](auto k) {  // registers, not a scratch-indexed array
-                  if (slot == decltype(k)::value) hz[decltype(k)::value] += zc;
-                });
-              }
+              if constexpr (HIST) codes[((((i - 1) & 1) * NCG + cg) * MT + m) * 64 + lane] = packed;
             }
           }
         }
       }
     }
+    if constexpr (HIST && TS == 1)
+      if (i >= 2) hist_count(hq_p, hq_y, hq_x, i & 1);  // tile i-2, stored in the last iteration
     if (i == ntile) break;
     if constexpr (!FUSE1) {
       if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
+    }
+    if constexpr (HIST) {
+      hq_p = ep_p;
+      hq_y = ep_y;
+      hq_x = ep_x;
     }
     tile_take(w_ep, ep_p, ep_y, ep_x);
     const char* buf = lds + (FUSE1 ? 0 : (i & 1)) * G::HALO_BYTES;
@@ -2044,12 +2066,15 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
   }
   range_report(a.rg, rmax);
-  if constexpr (HIST) {  // code-0 counts into bin 0, then the block's partial counts and plane ids
+  if constexpr (HIST) {  // the last tile's codes, code-0 counts into bin 0, then the partials
+    __syncthreads();
+    if constexpr (TS == 1)
+      if (ntile > 0) hist_count(ep_p, ep_y, ep_x, (ntile - 1) & 1);
     static_for<HIST_S>([&](auto k) {
       constexpr int K = decltype(k)::value;
       uint32_t z = hz[K];
       for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
-      if (TS == 0 && lane == 0 && z) atomicAdd(hist + K * 256 * HIST_R, z);
+      if (TS == 1 && lane == 0 && z) atomicAdd(hist + K * 256 * HIST_R, z);
     });
     __syncthreads();
     const int blk = a.ws_blk[model] + bi;  // the launch's block slot of the partials
