@@ -63,6 +63,7 @@ struct ConvArgs {
   // (nic_encode_entropy): per block [2 planes][256] partial counts and the 2 plane ids
   uint32_t* hist_part;
   int* hist_ids;
+  int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
   const uint16_t* wx2;

@@ -1707,7 +1707,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int ntot = np * per_plane;
   int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
   int walk_b = bi, walk_n = nb, hplane0 = 0;  // tile walk: start, stride; HIST: first plane
-  if constexpr (HIST) {  // bi = the block's group-relative index (not xcd_pos): its XCD range
+  if (HIST || a.ws2_xrange) {  // bi = the block's group-relative index (not xcd_pos): its XCD range
     long long st, len;
     int nx, j;
     hist_xcd_range(bi, nb, ntot, &st, &len, &nx, &j);
@@ -2516,7 +2516,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  const int bi = a.tile_xcd && !HIST ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
+  const int bi = a.tile_xcd && !HIST && !a.ws2_xrange ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
@@ -2752,6 +2752,9 @@ __global__ __launch_bounds__(256, 2) void dconv1_ws_kernel(ConvArgs a) {
 // outputs are bit-identical to dconv1_ws_kernel (GPU test).
 // ------------------------------------------------------------------------------------
 constexpr int D1A_LD = 2;  // code dwords per thread per tile (800 over 512 threads)
+#ifndef NIC_D1A_PF
+#define NIC_D1A_PF 2  // code prefetch distance in tiles (1: A/B build)
+#endif
 
 template <int KH1, int KW1, int TB1, int PY1, int PX1, int KH2, int KW2, int TB2, int PY2, int PX2>
 __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
@@ -2792,11 +2795,14 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     st_hx[j] = pix - (pix / 10) * 10;
     st_lds[j] = (pix / 10) * D1_RPB + st_hx[j] * D1_PSB + (q & 7) * 8;
   }
-  uint32_t cq[D1A_LD];
+  // codes of the next two tiles in registers (cqa: even tiles, cqb: odd), loaded two tiles
+  // ahead: one tile of MFMAs (~3.3k cycles per SIMD) did not cover the HBM latency of the next
+  // tile's code loads
+  uint32_t cqa[D1A_LD], cqb[D1A_LD];
   TileWalk it_ld, it_run;
   it_ld.init(bi, nb, a.tiles_y, a.tiles_x);
   it_run = it_ld;
-  auto load_codes = [&] {
+  auto load_codes = [&](uint32_t (&cq)[D1A_LD]) __attribute__((always_inline)) {
     int pl, ty, tx;
     it_ld.take(pl, ty, tx);
     const int p = p0 + pl;
@@ -2862,8 +2868,7 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
       __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), out_rs, in ? out_org + g_off[m] : kDmaOOR, 0, 0);
     }
   };
-  load_codes();
-  for (int i = 0; i < ntile; ++i) {
+  auto step = [&](int i, uint32_t (&cq)[D1A_LD]) __attribute__((always_inline)) {
     char* buf = lds + (i & 1) * D1_HB;
 #pragma unroll
     for (int j = 0; j < D1A_LD; ++j) {  // codes -> f16 (exact) in LDS
@@ -2877,9 +2882,23 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     stage_barrier();  // tile i's halo complete; tile i-2's reads of this buffer done everywhere
     int pl, ty, tx;
     it_run.take(pl, ty, tx);
-    if (i + 1 < ntile) load_codes();  // lands during this tile's MFMAs
+    if constexpr (NIC_D1A_PF == 2) {
+      if (i + 2 < ntile) load_codes(cq);  // tile i+2: lands during this tile's and the next's MFMAs
+    } else {  // A/B build: one tile ahead
+      if (i + 1 < ntile) load_codes(cq);
+    }
     phase(buf, &w1[0][0], std::integral_constant<int, KH1 * 4 + KW1>{}, PY1, PX1, p0 + pl, ty * 8, tx * 8);
     phase(buf, &w2[0][0], std::integral_constant<int, KH2 * 4 + KW2>{}, PY2, PX2, p0 + pl, ty * 8, tx * 8);
+  };
+  load_codes(cqa);
+  if constexpr (NIC_D1A_PF == 2) {
+    if (ntile > 1) load_codes(cqb);
+    for (int i = 0; i < ntile; i += 2) {
+      step(i, cqa);
+      if (i + 1 < ntile) step(i + 1, cqb);
+    }
+  } else {
+    for (int i = 0; i < ntile; ++i) step(i, cqa);
   }
   range_report(a.rg, rmax);
 }
@@ -5330,6 +5349,11 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   if constexpr (PIPE12) {
     hipLaunchKernelGGL(conv12_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   } else if constexpr (OUT_MODE == OUT_U8_LATENT && !FUSE1) {
+    static const bool xr = [] {
+      const char* e = getenv("NIC_C8W");
+      return e && e[0] == 'x';
+    }();
+    a.ws2_xrange = xr && !a.hist_part ? 1 : 0;
     if (a.hist_part) {
       if (!a.hist_ids || !hist_fold_supported(a.nimg, a.OH, a.OW)) return hipErrorInvalidValue;
       hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1, true>), dim3(a.ws_blk[2]), dim3(512), 0,
