@@ -317,9 +317,8 @@ struct nic_ctx {
   size_t ws_bytes = 0;
   uint32_t* counts = nullptr;
   size_t counts_bytes = 0;
-  // set only inside nic_encode_entropy: conv8's folded-histogram partials and plane ids
+  // set only inside nic_encode_entropy: conv8's folded-histogram partial counts
   uint32_t* fold_part = nullptr;
-  int* fold_ids = nullptr;
   char* qs = nullptr;  // MS-SSIM scratch (pooled scales + tile sums), grown on demand
   size_t qs_bytes = 0;
   // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
@@ -849,7 +848,6 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   a8.out_f32_latent = prequant;
   if (x3 && c->fold_part) {  // nic_encode_entropy: the split pass's conv8 counts the codes
     a8.hist_part = c->fold_part;
-    a8.hist_ids = c->fold_ids;
   }
   TIMED(L_CONV8, run(L_CONV8, a8));
   if (chained) HIP_TRY(launch_fp32_chain(chain, st));
@@ -1374,15 +1372,11 @@ int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint
   }
   int rc = grow_counts(c, hist_fold_scratch_bytes(n, h8, w8));
   if (rc) return rc;
-  // counts [blocks][slots][256], then ids [blocks][slots] (hist_fold_scratch_bytes)
-  const size_t fb = hist_fold_scratch_bytes(n, h8, w8);
-  c->fold_part = c->counts;
-  c->fold_ids = (int*)((char*)c->counts + fb / (256 * sizeof(uint32_t) + sizeof(int)) * 256 * sizeof(uint32_t));
+  c->fold_part = c->counts;  // [blocks][2 n planes][256] (hist_fold_scratch_bytes)
   rc = guarded(c, st, "nic_encode_entropy", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
     return encode_pass(c, rgb, n, h, w, latent, nullptr, st, x3, rg, timed);
   });
   c->fold_part = nullptr;
-  c->fold_ids = nullptr;
   if (rc) return rc;
   RangeGuard trip{};  // the split pass's epoch: a trip means the re-run rewrote the latent
   trip.flag = c->range;

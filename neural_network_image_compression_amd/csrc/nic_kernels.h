@@ -59,10 +59,9 @@ struct ConvArgs {
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
   int ws_xcd;             // weight-stationary kernels: logical block = XCD-contiguous remap of blockIdx
   int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
-  // conv8 (f16x3, OUT_U8_LATENT) with the latent histogram folded into its epilogue
-  // (nic_encode_entropy): per block [2 planes][256] partial counts and the 2 plane ids
+  // conv8 (f16x3, OUT_U8_LATENT) with the latent histogram folded in (nic_encode_entropy):
+  // per block and plane of its group the partial counts [block][2 nimg][256]
   uint32_t* hist_part;
-  int* hist_ids;
   int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment

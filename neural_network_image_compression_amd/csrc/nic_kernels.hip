@@ -1660,23 +1660,23 @@ constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
 // the last column read a finite 0 for the zero weight of kw = 5
 constexpr int C12_PP = 52;
 
-// HIST (conv8 in nic_encode_entropy): the ts = 0 epilogue also counts the u8 codes into
-// per-block LDS histograms [HIST_S planes][256][HIST_R replicas] (code 0 counted per lane in
-// registers: trained latents are mostly zeros), written out as partial counts + plane ids at
-// the end (hist_fold_kernel reduces them).  So that a block meets at most HIST_S planes, the
-// group's tiles are cut into one contiguous range per XCD (in proportion to its blocks) and
-// the XCD's blocks stride through their range -- at each step an XCD still works on a
-// contiguous strip of tiles (shared halo rows / columns in its L2), as the default walk does.
-// (A contiguous range per block, ~two planes: conv8 0.891 -> 1.069 ms on 4K frames, the halo
-// sharing between concurrently running neighbour tiles lost.)
-constexpr int HIST_R = 2, HIST_S = 4;
-// + the codes of the last two tiles ([2 parities][NCG][MT][64 lanes] u32, conv8: 2 KB): the
-// ts = 0 epilogue stores them, the ts = 1 waves (which wait ~1,700 cycles per tile at the top
-// barrier, tools/c8_stamps.cpp) count them one tile later -- counting in the ts = 0 epilogue
-// itself lengthened the critical pair of waves (conv8 +12 % on 4K frames)
-constexpr int HIST_LDS = HIST_S * 256 * HIST_R * 4 + 2 * 2 * 2 * 64 * 4;
+// HIST (conv8 in nic_encode_entropy): the latent histogram counted inside conv8.  The ts = 0
+// epilogue stores each tile's packed codes in LDS; the ts = 1 waves (idle ~1,700 cycles per
+// tile at the top barrier, tools/c8_stamps.cpp) count them one tile later into a per-block LDS
+// histogram [256][HIST_R replicas] (code 0 counted per lane in a register: trained latents are
+// mostly zeros).  The block keeps the default strided walk (tiles bi, bi + nb, ...: the XCD-
+// contiguous strips of xcd_pos), whose planes are visited in order, one after the other, so two
+// LDS histograms alternate by plane parity: when the counted plane changes, the finished one is
+// written out as the block's partial counts of that plane one tile later and cleared
+// (hist_fold_kernel adds the blocks' partials per plane).  Needs >= 2 tiles per plane per block
+// (nb <= tiles per plane / 2: large frames, config 5; hist_fold_supported).
+// Measured against other forms (4K frames, conv8 alone 0.891-0.900 ms): counting in the ts = 0
+// epilogue lengthened the critical pair of waves, and walks that give a block fewer planes
+// (a contiguous range per block: 1.069 ms; per XCD: 0.952 ms) lose the strip locality.
+constexpr int HIST_R = 2;
+constexpr int HIST_LDS = 2 * 256 * HIST_R * 4 + 2 * 2 * 2 * 64 * 4;  // + codes [2][NCG][MT][64] (conv8)
 __host__ __device__ inline void hist_xcd_range(int rel, int nb, long long ntot, long long* start, long long* len, int* nx,
-                                               int* j) {
+                                               int* j) {  // A/B walk (NIC_C8W=x): one tile range per XCD
   const int x = rel & 7, q = nb >> 3, r = nb & 7;
   const int px = x * q + (x < r ? x : r);  // first position of XCD class x (xcd_pos)
   *nx = q + (x < r ? 1 : 0);
@@ -1706,25 +1706,53 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
   int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
-  int walk_b = bi, walk_n = nb, hplane0 = 0;  // tile walk: start, stride; HIST: first plane
-  if (HIST || a.ws2_xrange) {  // bi = the block's group-relative index (not xcd_pos): its XCD range
+  int walk_b = bi, walk_n = nb;  // tile walk: start, stride
+  if (!HIST && a.ws2_xrange) {   // A/B: bi = the block's group-relative index, its XCD range
     long long st, len;
     int nx, j;
     hist_xcd_range(bi, nb, ntot, &st, &len, &nx, &j);
     walk_b = (int)(st + j);
     walk_n = nx;
     ntile = j < len ? (int)((len - j + nx - 1) / nx) : 0;
-    hplane0 = p0 + (int)((st + j) / per_plane);
   }
-  uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [HIST_S][256][HIST_R]
-  uint32_t* codes = hist + HIST_S * 256 * HIST_R;                    // HIST: [2][NCG][MT][64]
-  uint32_t hz[HIST_S] = {};  // HIST: this lane's code-0 counts per plane slot
-  int hq_p = 0, hq_y = 0, hq_x = 0;  // HIST: the tile whose codes the ts = 1 waves count next
-  // HIST, ts = 1: count the codes the ts = 0 wave of this cg stored for tile (p, y, x)
+  uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [2 parities][256][HIST_R]
+  uint32_t* codes = hist + 2 * 256 * HIST_R;                         // HIST: [2][NCG][MT][64]
+  // HIST, ts = 1 waves: the plane (group-local) being counted, its code-0 count in this lane,
+  // the plane whose histogram waits to be written out (-1: none), the tile to count next
+  int hcur = 0, hpend = -1;
+  uint32_t hz = 0;
+  int hq_p = 0, hq_y = 0, hq_x = 0;
+  const int hblk = blockIdx.x;  // partial row of this block (a group's blocks are contiguous)
+  auto hist_flush = [&](int q) __attribute__((always_inline)) {  // both ts = 1 waves, 128 bins each
+    uint32_t* hb = hist + (q & 1) * (256 * HIST_R);
+    const int t = cg * 64 + lane;  // cg 0, 1 of the ts = 1 waves (NCG = 2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int bin = t + 128 * h;
+      uint32_t c = 0;
+#pragma unroll
+      for (int r = 0; r < HIST_R; ++r) {
+        c += hb[bin * HIST_R + r];
+        hb[bin * HIST_R + r] = 0;
+      }
+      a.hist_part[((size_t)hblk * 2 * a.nimg + q) * 256 + bin] = c;
+    }
+  };
+  auto hist_close = [&] __attribute__((always_inline)) {  // this wave's code-0 count of hcur into bin 0
+    uint32_t z = hz;
+    for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
+    if (lane == 0 && z) atomicAdd(hist + (hcur & 1) * (256 * HIST_R), z);
+    hz = 0;
+  };
+  // count the codes the ts = 0 wave of this cg stored for tile (p, y, x) (code buffer par)
   auto hist_count = [&](int p, int ty0, int tx0, int par) __attribute__((always_inline)) {
-    const int slot = p - hplane0;  // wave-uniform, < HIST_S (hist_fold_supported)
-    uint32_t* hs = hist + slot * (256 * HIST_R) + (lane & (HIST_R - 1));
-    uint32_t zc = 0;
+    const int q = p - p0;  // wave-uniform; planes come in order
+    if (q != hcur) {
+      hist_close();
+      hpend = hcur;
+      hcur = q;
+    }
+    uint32_t* hs = hist + (q & 1) * (256 * HIST_R) + (lane & (HIST_R - 1));
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int oy = ty0 + 2 * m + (l16 >> 3), ox = tx0 + (l16 & 7);
@@ -1734,15 +1762,12 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         for (int r = 0; r < 4; ++r) {
           const uint32_t code = (w >> (8 * r)) & 255;
           if (code == 0)
-            ++zc;
+            ++hz;
           else
             atomicAdd(hs + code * HIST_R, 1u);
         }
       }
     }
-    static_for<HIST_S>([&](auto k) {  // registers, not a scratch-indexed array
-      if (slot == decltype(k)::value) hz[decltype(k)::value] += zc;
-    });
   };
 
   f16x8 wr[NT][KST][2];
@@ -1770,7 +1795,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   w_issue.init(walk_b, walk_n, a.tiles_y, a.tiles_x);
   w_ep = w_rgb = w_issue;
   if constexpr (HIST)
-    for (int q = threadIdx.x; q < HIST_S * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
+    for (int q = threadIdx.x; q < 2 * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
   auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
     int pl, ty, tx;
     w.take(pl, ty, tx);
@@ -1931,8 +1956,13 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         }
       }
     }
-    if constexpr (HIST && TS == 1)
+    if constexpr (HIST && TS == 1) {
+      if (hpend >= 0) {  // both ts = 1 waves closed it before this barrier
+        hist_flush(hpend);
+        hpend = -1;
+      }
       if (i >= 2) hist_count(hq_p, hq_y, hq_x, i & 1);  // tile i-2, stored in the last iteration
+    }
     if (i == ntile) break;
     if constexpr (!FUSE1) {
       if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
@@ -2066,28 +2096,20 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
   }
   range_report(a.rg, rmax);
-  if constexpr (HIST) {  // the last tile's codes, code-0 counts into bin 0, then the partials
+  if constexpr (HIST) {  // the last tile's codes, then the last planes' partial counts
     __syncthreads();
-    if constexpr (TS == 1)
+    if constexpr (TS == 1) {
+      if (hpend >= 0) {
+        hist_flush(hpend);
+        hpend = -1;
+      }
       if (ntile > 0) hist_count(ep_p, ep_y, ep_x, (ntile - 1) & 1);
-    static_for<HIST_S>([&](auto k) {
-      constexpr int K = decltype(k)::value;
-      uint32_t z = hz[K];
-      for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o);
-      if (TS == 1 && lane == 0 && z) atomicAdd(hist + K * 256 * HIST_R, z);
-    });
-    __syncthreads();
-    const int blk = a.ws_blk[model] + bi;  // the launch's block slot of the partials
-    for (int q = threadIdx.x; q < HIST_S * 256; q += 64 * NW) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int r = 0; r < HIST_R; ++r) c += hist[q * HIST_R + r];
-      a.hist_part[(size_t)blk * HIST_S * 256 + q] = c;
+      hist_close();
     }
-    if (threadIdx.x < HIST_S) {
-      const int last = ntile > 0 ? p0 + (int)(((long long)walk_b + (long long)(ntile - 1) * walk_n) / per_plane) : -1;
-      const int pid = hplane0 + (int)threadIdx.x;
-      a.hist_ids[blk * HIST_S + threadIdx.x] = ntile > 0 && pid <= last ? pid : -1;
+    __syncthreads();
+    if constexpr (TS == 1) {
+      if (hpend >= 0) hist_flush(hpend);
+      if (ntile > 0) hist_flush(hcur);
     }
   }
 #ifdef NIC_STAMPS
@@ -2516,7 +2538,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  const int bi = a.tile_xcd && !HIST && !a.ws2_xrange ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
+  const int bi = a.tile_xcd && !a.ws2_xrange ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
@@ -4779,8 +4801,8 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
 // blocks follow from the contiguous ranges).  If the split pass tripped the range guard, the
 // latent was rewritten by the exact-fp32 re-run after conv8 counted: the plane is recounted
 // from z (LDS atomics; the rare path).
-__global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restrict__ part, const int* __restrict__ ids,
-                                                        int nimg, int per_plane, int by, int bc,
+__global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restrict__ part, int nimg, int per_plane,
+                                                        int by, int bc,
                                                         const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
                                                         float n_sym, uint32_t* __restrict__ counts,
                                                         float* __restrict__ bits) {
@@ -4789,12 +4811,9 @@ __global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restri
   const int p = blockIdx.x, bin = threadIdx.x;
   const bool tripped = trip.flag && *(volatile const int*)trip.flag == trip.epoch;
   uint32_t c = 0;
-  if (!tripped) {  // every block of the plane's group, every slot whose id is p (fixed order)
-    const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0;
-    for (int b = base; b < base + nb; ++b)
-#pragma unroll
-      for (int s = 0; s < HIST_S; ++s)
-        if (ids[b * HIST_S + s] == p) c += part[((size_t)b * HIST_S + s) * 256 + bin];
+  if (!tripped) {  // every block of the plane's group wrote its partial counts of the plane
+    const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0, q = p - (gi ? nimg : 0);
+    for (int b = base; b < base + nb; ++b) c += part[((size_t)b * 2 * nimg + q) * 256 + bin];
   } else {
     h[bin] = 0;
     __syncthreads();
@@ -5301,32 +5320,22 @@ static void ws2_groups(int nimg, long long per_plane, int* by, int* bc) {
   *bc = (int)std::max(1LL, std::min((long long)target - y, tc));
 }
 
-// conv8's tile grid (4 x 8 output tiles) and the fold's condition: every XCD range of tiles
-// (hist_xcd_range) spans at most HIST_S planes -- large frames (config 5: 2 XCD ranges per
-// 4K plane); batches of small images run the two-call form
+// conv8's tile grid (4 x 8 output tiles) and the fold's condition: every block meets each plane
+// of its group in >= 2 consecutive tiles (group blocks <= tiles per plane / 2) -- large frames
+// (config 5); batches of small images run the two-call form
 bool hist_fold_supported(int nimg, int h8, int w8) {
   if (nimg <= 0 || h8 <= 0 || w8 <= 0) return false;
   const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  for (int gi = 0; gi < 2; ++gi) {
-    const int nb = gi ? bc : by;
-    const long long ntot = pp * (gi ? 2 : 1) * nimg;
-    for (int x = 0; x < 8 && x < nb; ++x) {
-      long long st, len;
-      int nx, j;
-      hist_xcd_range(x, nb, ntot, &st, &len, &nx, &j);
-      if (len > 0 && (st + len - 1) / pp - st / pp + 1 > HIST_S) return false;
-    }
-  }
-  return true;
+  return 2LL * by <= pp && 2LL * bc <= pp;
 }
 
-size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {
+size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {  // [block][2 nimg planes][256]
   const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  return (size_t)(by + bc) * HIST_S * (256 * sizeof(uint32_t) + sizeof(int));
+  return (size_t)(by + bc) * 2 * nimg * 256 * sizeof(uint32_t);
 }
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
@@ -5355,7 +5364,7 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
     }();
     a.ws2_xrange = xr && !a.hist_part ? 1 : 0;
     if (a.hist_part) {
-      if (!a.hist_ids || !hist_fold_supported(a.nimg, a.OH, a.OW)) return hipErrorInvalidValue;
+      if (!hist_fold_supported(a.nimg, a.OH, a.OW)) return hipErrorInvalidValue;
       hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1, true>), dim3(a.ws_blk[2]), dim3(512), 0,
                          st, a);
     } else {
@@ -5653,8 +5662,7 @@ hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, in
   const int pp = ((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  const int* ids = (const int*)(part + (size_t)(by + bc) * HIST_S * 256);
-  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, ids, nimg, pp, by, bc, z, h8 * w8, trip,
+  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, nimg, pp, by, bc, z, h8 * w8, trip,
                      (float)h8 * w8 * 32.0f, counts, bits);
   return hipGetLastError();
 }

@@ -262,15 +262,15 @@ def test_entropy_matches_golden(case, codecs, golden):
     np.testing.assert_allclose(bits.cpu().numpy(), g["bits"].ravel(), rtol=0, atol=2e-6)
 
 
-@pytest.mark.parametrize("shape", [(64, 256, 256), (2, 2160, 3840), (8, 2160, 3840), (4, 128, 128), (3, 37, 53),
-                                   (1, 8, 8), (2, 1, 2400), (1000, 8, 8)],
-                         ids=["config2-two-call", "4k", "4k-config5", "imagenet", "odd", "tiny", "one-row",
-                              "many-tiny-two-call"])
+@pytest.mark.parametrize("shape", [(2, 2160, 3840), (8, 2160, 3840), (1, 1080, 1921), (64, 256, 256), (4, 128, 128),
+                                   (3, 37, 53), (2, 1, 2400), (1000, 8, 8)],
+                         ids=["4k", "4k-config5", "fhd-odd-edges", "config2-two-call", "imagenet-two-call",
+                              "odd-two-call", "one-row-two-call", "many-tiny-two-call"])
 def test_encode_entropy_fold(shape, weights_spread, weights_trained):
     """nic_encode_entropy (the latent histogram counted in conv8's epilogue, BASELINE config 5)
     against nic_encode + nic_entropy_hist: latent, counts and bits bit-exact, with seeded and
-    trained (zero-heavy latents) weights; shapes whose XCD tile ranges would span more than
-    HIST_S planes take the two-call path (*-two-call); counts also equal the oracle's."""
+    trained (zero-heavy latents) weights; shapes with fewer than two tiles per plane per conv8
+    block take the two-call path (*-two-call); counts also equal the oracle's."""
     from neural_network_image_compression_amd.codec import Codec
     n, h, w = shape
     x = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(n * h + w))
