@@ -1721,7 +1721,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   // the plane whose histogram waits to be written out (-1: none), the tile to count next
   int hcur = 0, hpend = -1;
   uint32_t hz = 0;
-  int hq_p = 0, hq_y = 0, hq_x = 0;
+  int h1_p = 0, h1_y = 0, h1_x = 0, h2_p = 0, h2_y = 0, h2_x = 0;  // tiles i-1, i-2 (after tile_take)
   const int hblk = blockIdx.x;  // partial row of this block (a group's blocks are contiguous)
   auto hist_flush = [&](int q) __attribute__((always_inline)) {  // both ts = 1 waves, 128 bins each
     uint32_t* hb = hist + (q & 1) * (256 * HIST_R);
@@ -1956,21 +1956,17 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         }
       }
     }
-    if constexpr (HIST && TS == 1) {
-      if (hpend >= 0) {  // both ts = 1 waves closed it before this barrier
-        hist_flush(hpend);
-        hpend = -1;
-      }
-      if (i >= 2) hist_count(hq_p, hq_y, hq_x, i & 1);  // tile i-2, stored in the last iteration
-    }
     if (i == ntile) break;
     if constexpr (!FUSE1) {
       if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
     }
     if constexpr (HIST) {
-      hq_p = ep_p;
-      hq_y = ep_y;
-      hq_x = ep_x;
+      h2_p = h1_p;
+      h2_y = h1_y;
+      h2_x = h1_x;
+      h1_p = ep_p;
+      h1_y = ep_y;
+      h1_x = ep_x;
     }
     tile_take(w_ep, ep_p, ep_y, ep_x);
     const char* buf = lds + (FUSE1 ? 0 : (i & 1)) * G::HALO_BYTES;
@@ -2094,6 +2090,15 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 #pragma unroll
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
     }
+    // HIST: the ts = 1 waves count after their own MFMA stream, where they would wait at the
+    // next barrier: tile i-2's codes (stored by ts = 0 at the top of iteration i-1)
+    if constexpr (HIST && TS == 1) {
+      if (hpend >= 0) {  // both ts = 1 waves closed it before this iteration's barrier
+        hist_flush(hpend);
+        hpend = -1;
+      }
+      if (i >= 2) hist_count(h2_p, h2_y, h2_x, i & 1);
+    }
   }
   range_report(a.rg, rmax);
   if constexpr (HIST) {  // the last tile's codes, then the last planes' partial counts
@@ -2103,7 +2108,8 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         hist_flush(hpend);
         hpend = -1;
       }
-      if (ntile > 0) hist_count(ep_p, ep_y, ep_x, (ntile - 1) & 1);
+      if (ntile > 1) hist_count(h1_p, h1_y, h1_x, (ntile - 2) & 1);  // tile ntile-2
+      if (ntile > 0) hist_count(ep_p, ep_y, ep_x, (ntile - 1) & 1);  // tile ntile-1
       hist_close();
     }
     __syncthreads();
