@@ -4807,33 +4807,46 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
 // blocks follow from the contiguous ranges).  If the split pass tripped the range guard, the
 // latent was rewritten by the exact-fp32 re-run after conv8 counted: the plane is recounted
 // from z (LDS atomics; the rare path).
-__global__ __launch_bounds__(256) void hist_fold_kernel(const uint32_t* __restrict__ part, int nimg, int per_plane,
-                                                        int by, int bc,
-                                                        const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
-                                                        float n_sym, uint32_t* __restrict__ counts,
-                                                        float* __restrict__ bits) {
-  __shared__ uint32_t h[256];
+// 1024 threads per plane: 4 groups of 256 bins, each summing every 4th block's partial (8 loads
+// in flight per thread), met in LDS -- the plane's ~85-171 partials of 1 KB are read in a few
+// latency rounds instead of one after the other.
+__global__ __launch_bounds__(1024) void hist_fold_kernel(const uint32_t* __restrict__ part, int nimg, int per_plane,
+                                                         int by, int bc,
+                                                         const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
+                                                         float n_sym, uint32_t* __restrict__ counts,
+                                                         float* __restrict__ bits) {
+  __shared__ uint32_t h[4][256];
   __shared__ double red[4];
-  const int p = blockIdx.x, bin = threadIdx.x;
+  const int p = blockIdx.x, bin = threadIdx.x & 255, grp = threadIdx.x >> 8;
   const bool tripped = trip.flag && *(volatile const int*)trip.flag == trip.epoch;
-  uint32_t c = 0;
   if (!tripped) {  // every block of the plane's group wrote its partial counts of the plane
     const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0, q = p - (gi ? nimg : 0);
-    for (int b = base; b < base + nb; ++b) c += part[((size_t)b * 2 * nimg + q) * 256 + bin];
+    const uint32_t* src = part + ((size_t)base * 2 * nimg + q) * 256 + bin;
+    const size_t bstride = (size_t)2 * nimg * 256;
+    uint32_t acc[8] = {};
+    for (int b0 = grp; b0 < nb; b0 += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + 4 * u;
+        if (b < nb) acc[u] += src[(size_t)b * bstride];
+      }
+    }
+    h[grp][bin] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   } else {
-    h[bin] = 0;
+    if (grp == 0) h[0][bin] = 0;
     __syncthreads();
     const int n = p % nimg, type = p / nimg;
     const uint8_t* src = z + (size_t)n * plane_px * 96 + type * 32;
-    for (long long i = bin; i < (long long)plane_px * 8; i += 256) {
+    for (long long i = threadIdx.x; i < (long long)plane_px * 8; i += 1024) {
       const uint32_t w = *(const uint32_t*)(src + (i >> 3) * 96 + (i & 7) * 4);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) atomicAdd(&h[(w >> (8 * k)) & 255], 1u);
+      for (int k = 0; k < 4; ++k) atomicAdd(&h[0][(w >> (8 * k)) & 255], 1u);
     }
-    __syncthreads();
-    c = h[bin];
+    if (grp > 0) h[grp][bin] = 0;
   }
-  plane_entropy(c, bin, p, n_sym, counts, bits, red);
+  __syncthreads();
+  const uint32_t c = threadIdx.x < 256 ? (h[0][bin] + h[1][bin]) + (h[2][bin] + h[3][bin]) : 0u;
+  plane_entropy(c, threadIdx.x, p, n_sym, counts, bits, red);
 }
 
 __global__ __launch_bounds__(256) void pack_latent_kernel(const uint8_t* __restrict__ z, uint8_t* __restrict__ out,
@@ -5668,7 +5681,7 @@ hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, in
   const int pp = ((h8 + 3) / 4) * ((w8 + 7) / 8);
   int by, bc;
   ws2_groups(nimg, pp, &by, &bc);
-  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, nimg, pp, by, bc, z, h8 * w8, trip,
+  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, nimg, pp, by, bc, z, h8 * w8, trip,
                      (float)h8 * w8 * 32.0f, counts, bits);
   return hipGetLastError();
 }
