@@ -2154,6 +2154,12 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 constexpr int C12_PPW = 21;                          // patch row pitch in dwords (42 f16 columns)
 constexpr int C12_PPIECE = (C12_PH * C12_PPW + 63) / 64;  // 1-dword-per-lane DMA pieces per plane (14)
 constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in LDS (hi or lo)
+#ifndef NIC_C12_E3
+// 1: pixel tile MT-1's conv2 epilogue runs on the ts 1 wave (at the top of the next tile, from
+// its own sums kept in registers and the ts 0 wave's sums of that tile left in LDS) instead of
+// on the ts 0 wave; 0: every epilogue on ts 0 (A/B build)
+#define NIC_C12_E3 1
+#endif
 #ifndef NIC_C12_PT0
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
@@ -2211,6 +2217,9 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   char* part = lds + 2 * G::HALO_BYTES;           // [NCG] partial tiles of the ts = 1 waves
   char* patches = part + NCG * PART;              // [2 parities][hi, lo] patch planes
   int* pflag = (int*)(patches + 4 * C12_PLANE);   // [NCG] last tile whose partials ts 0 has read
+  // NIC_C12_E3: the ts 0 waves' sums of pixel tile MT-1 for the ts 1 wave [2 parities][NCG][1 KB]
+  char* part3 = (char*)(pflag + 4);
+  constexpr int E_MT = NIC_C12_E3 ? MT - 1 : MT;  // pixel tiles whose epilogue ts 0 runs
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -2402,15 +2411,19 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     __builtin_amdgcn_s_setprio(0);
   };
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
-  auto epilogue = [&](int i) {  // ts 0: own sums + the ts 1 partials, bias, leaky, split, 16-B stores
+  // epilogue of tile i (called for i = 0, 1, 2, ... in order by each role): ts 0 runs pixel
+  // tiles [0, E_MT) from its own sums + the ts 1 partials; with NIC_C12_E3 the ts 1 wave runs
+  // pixel tile MT-1 from its own sums + the ts 0 sums in part3 (a + b == b + a: same bits)
+  auto epilogue = [&](int i) {
     int p, t0y, t0x;
-    tile_take(w_ep, p, t0y, t0x);  // epilogue is called for i = 0, 1, 2, ... in order
-    const char* pp = part + cg * PART + lane * 16;
+    tile_take(w_ep, p, t0y, t0x);
+    constexpr int M0 = TS == 0 ? 0 : E_MT, M1 = TS == 0 ? E_MT : MT;
+    const char* pp = TS == 0 ? part + cg * PART + lane * 16 : part3 + ((i & 1) * NCG + cg) * 1024 + lane * 16 - M0 * 1024;
     f32x4 q4[MT];  // all partial reads in flight before the first use
 #pragma unroll
-    for (int m = 0; m < MT; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
+    for (int m = M0; m < M1; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
+    for (int m = M0; m < M1; ++m) {
       const f32x4 q = q4[m];
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
@@ -2475,8 +2488,12 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
       stream(i);
+      if constexpr (NIC_C12_E3)  // this wave's sums of pixel tile MT-1 for the ts 1 wave
+        *(f32x4*)(part3 + ((i & 1) * NCG + cg) * 1024 + lane * 16) = acc[MT - 1];
       C12_MARK(5);
     } else {
+      if constexpr (NIC_C12_E3)
+        if (i > 0) epilogue(i - 1);  // pixel tile MT-1 of tile i-1 (its sums still in acc)
       if (i == ntile) break;
       if (i + 2 < ntile) patch_dma(i + 2);  // into the buffer conv1(i) read; lands during the stream
       C12_MARK(4);
@@ -2488,7 +2505,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       C12_MARK(2);
       char* pp = part + cg * PART + lane * 16;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+      for (int m = 0; m < E_MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
       dma_wait_all();  // patch i+2 landed (before B_top(i+1) publishes it)
@@ -2521,7 +2538,8 @@ __device__ __forceinline__ int xcd_pos(int b, int nb) {
 
 __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
   using G = GeomS2<32, 8, 8>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16];
+  __shared__ __attribute__((aligned(16)))
+  char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16 + (NIC_C12_E3 ? 2 * 4 * 1024 : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
