@@ -2155,10 +2155,13 @@ constexpr int C12_PPW = 21;                          // patch row pitch in dword
 constexpr int C12_PPIECE = (C12_PH * C12_PPW + 63) / 64;  // 1-dword-per-lane DMA pieces per plane (14)
 constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in LDS (hi or lo)
 #ifndef NIC_C12_E3
-// 1: pixel tile MT-1's conv2 epilogue runs on the ts 1 wave (at the top of the next tile, from
-// its own sums kept in registers and the ts 0 wave's sums of that tile left in LDS) instead of
-// on the ts 0 wave; 0: every epilogue on ts 0 (A/B build)
-#define NIC_C12_E3 1
+// 1 (A/B build): pixel tile MT-1's conv2 epilogue runs on the ts 1 wave (at the top of the next
+// tile, from its own sums kept in registers and the ts 0 wave's sums of that tile left in LDS)
+// instead of on the ts 0 wave, whose chain is the longer one by stamps (7,843 vs 6,734 cycles
+// per tile, profiles/r3n_c12_stamps.txt).  Measured slower: conv12 0.236-0.238 vs 0.228-0.230
+// ms (3 alternating rounds), 4K 3.89 vs 3.62 ms (profiles/r4_ab_logs.txt) -- the ts 1 wave's
+// patch DMA and stream start later, and that delay reaches the next barrier.
+#define NIC_C12_E3 0
 #endif
 #ifndef NIC_C12_PT0
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
