@@ -24,6 +24,9 @@
 // libpng does), IDAT chunks of libpng's 8,192-byte zbuffer, no ancillary chunks.  TensorFlow
 // is not importable here, so this mode is a restatement of those libraries' published
 // behaviour: parity with TF's own output is unpinned.
+// Byte equality with Pillow also assumes the deflate Pillow links is the same algorithm as the
+// system zlib this library links (-lz): true for the image's Pillow (tests/test_png_encode.py
+// compares the files); a Pillow built on zlib-ng or libdeflate would choose other matches.
 // One image per task, a fixed pool of std::threads, no Python.
 #include <zlib.h>
 
