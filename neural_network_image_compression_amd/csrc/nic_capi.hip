@@ -325,8 +325,19 @@ struct nic_ctx {
   // call, read back and accumulated by nic_layer_times
   // host-array surface (nic_encode_host / nic_decode_host): its own copy-in, compute and
   // copy-out streams, per-chunk events, pinned staging and device buffers, grown on demand
-  hipStream_t hs[3] = {};
+  hipStream_t hs[4] = {};  // H2D, compute (even chunks), D2H, compute (odd chunks)
   hipEvent_t hev[3][kHostMaxChunks] = {};
+  // the odd chunks' pass state (activation regions, range-guard words and epoch): swapped into
+  // ws / ws_bytes / range / epoch around their launches, so two chunk passes can run at once on
+  // the two compute streams (host_pipeline)
+  struct PassSlot {
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    int* range = nullptr;
+    int epoch = 0;
+  } alt;
+  int* alt_host = nullptr;  // pinned read-back of alt.range
+  hipEvent_t hev_alt = nullptr;  // alt.range's read-back done
   hipEvent_t hev_caller = nullptr;
   uint8_t* pin_in = nullptr;
   uint8_t* pin_out = nullptr;
@@ -590,15 +601,19 @@ int nic_destroy(nic_ctx* c) {
   if (c->wproj) (void)hipFree(c->wproj);
   if (c->range) (void)hipFree(c->range);
   if (c->range_host) (void)hipHostFree(c->range_host);
+  if (c->alt.ws) (void)hipFree(c->alt.ws);
+  if (c->alt.range) (void)hipFree(c->alt.range);
+  if (c->alt_host) (void)hipHostFree(c->alt_host);
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 3; ++i)
     for (int k = 0; k < kHostMaxChunks; ++k)
       if (c->hev[i][k]) (void)hipEventDestroy(c->hev[i][k]);
+  for (int i = 0; i < 4; ++i)
     if (c->hs[i]) (void)hipStreamDestroy(c->hs[i]);
-  }
   if (c->hev_caller) (void)hipEventDestroy(c->hev_caller);
+  if (c->hev_alt) (void)hipEventDestroy(c->hev_alt);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->hdev) (void)hipFree(c->hdev);
@@ -964,6 +979,14 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
 // run the exact-fp32 kernels (64-bit addressing) instead of failing (nic.h).
 bool x3_plane_fits(long long h64, long long w64) { return h64 * w64 * 64 * 4 < (1LL << 30); }
 
+// Swap the host pipeline's second pass slot into (or back out of) the ctx fields the passes use.
+void swap_slot(nic_ctx* c) {
+  std::swap(c->ws, c->alt.ws);
+  std::swap(c->ws_bytes, c->alt.ws_bytes);
+  std::swap(c->range, c->alt.range);
+  std::swap(c->epoch, c->alt.epoch);
+}
+
 // The chained re-run's barrier timeout (nic_kernels.hip grid_barrier), read from words[4] of
 // c->range with the device idle: reported once as NIC_EHIP, and the barrier words (arrivals,
 // generation, flag) are zeroed so the next chain starts clean (an abandoned barrier leaves
@@ -1126,6 +1149,15 @@ class CopyPool {
   std::condition_variable cv_;
 };
 
+// NIC_HOST_SLOTS=1 (A/B): every chunk pass on one compute stream and one pass slot
+bool host_two_slots() {
+  static const bool on = [] {
+    const char* e = getenv("NIC_HOST_SLOTS");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 // Host-side wait for an event: polling hipEventQuery (default) returns as soon as the GPU
 // signals, where hipEventSynchronize may sleep and pay a wake-up latency per chunk
 // (NIC_HOST_SPIN=0 for the runtime's wait).
@@ -1143,12 +1175,20 @@ hipError_t host_wait(hipEvent_t e) {
 }
 
 int host_setup(nic_ctx* c) {
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i)
     if (!c->hs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking));
+  for (int i = 0; i < 3; ++i)
     for (int k = 0; k < kHostMaxChunks; ++k)
       if (!c->hev[i][k]) HIP_TRY(hipEventCreateWithFlags(&c->hev[i][k], hipEventDisableTiming));
-  }
   if (!c->hev_caller) HIP_TRY(hipEventCreateWithFlags(&c->hev_caller, hipEventDisableTiming));
+  if (!c->hev_alt) HIP_TRY(hipEventCreateWithFlags(&c->hev_alt, hipEventDisableTiming));
+  if (!c->alt.range) {
+    if (hipMalloc(&c->alt.range, 8 * sizeof(int)) != hipSuccess || hipMemset(c->alt.range, 0, 8 * sizeof(int)) != hipSuccess ||
+        hipHostMalloc(&c->alt_host, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(NIC_ENOMEM, "host surface: second pass slot allocation failed");
+    }
+  }
   return NIC_OK;
 }
 
@@ -1180,9 +1220,14 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   std::vector<int> lo;
   host_chunk_plan(n, chunks, lo);
   const int K = (int)lo.size() - 1;
+  // odd chunks on the second compute stream with the second pass slot: a chunk's kernels fill
+  // the tails of the previous chunk's (one stream serialised them: ~0.1 ms per call at config 2)
+  const bool two = host_two_slots() && K > 1;
+  hipStream_t cs[2] = {c->hs[1], two ? c->hs[3] : c->hs[1]};
   HIP_TRY(hipEventRecord(c->hev_caller, caller));
   HIP_TRY(hipStreamWaitEvent(c->hs[0], c->hev_caller, 0));
   HIP_TRY(hipStreamWaitEvent(c->hs[1], c->hev_caller, 0));
+  if (two) HIP_TRY(hipStreamWaitEvent(c->hs[3], c->hev_caller, 0));
   int err = NIC_OK, issued = 0;
   for (int k = 0; k < K && !err; ++k) {
     const size_t i0 = lo[k] * in_row, ib = (lo[k + 1] - lo[k]) * in_row;
@@ -1192,16 +1237,19 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
       CopyPool::get().copy(c->pin_in + i0, in + i0, ib);
       src = c->pin_in + i0;
     }
+    const int sl = two ? (k & 1) : 0;
     hipError_t e = hipMemcpyAsync(d_in + i0, src, ib, hipMemcpyHostToDevice, c->hs[0]);
     if (e == hipSuccess) e = hipEventRecord(c->hev[0][k], c->hs[0]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[1], c->hev[0][k], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs[sl], c->hev[0][k], 0);
     if (e != hipSuccess) {
       err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
       break;
     }
-    err = pass(d_in + i0, lo[k + 1] - lo[k], d_out + o0, c->hs[1]);
+    if (sl) swap_slot(c);
+    err = pass(d_in + i0, lo[k + 1] - lo[k], d_out + o0, cs[sl]);
+    if (sl) swap_slot(c);
     if (err) break;
-    e = hipEventRecord(c->hev[1][k], c->hs[1]);
+    e = hipEventRecord(c->hev[1][k], cs[sl]);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[2], c->hev[1][k], 0);
     if (e == hipSuccess)
       e = hipMemcpyAsync(out_pin ? out + o0 : c->pin_out + o0, d_out + o0, ob, hipMemcpyDeviceToHost, c->hs[2]);
@@ -1217,7 +1265,9 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   const bool chain_check = !err && issued > 0 && c->precision == NIC_PRECISION_F16X3 &&
                            c->range_policy == NIC_RANGE_FALLBACK;
   if (chain_check && (hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess ||
-                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess))
+                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess ||
+                      (two && (hipMemcpyAsync(c->alt_host, c->alt.range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[3]) != hipSuccess ||
+                               hipEventRecord(c->hev_alt, c->hs[3]) != hipSuccess))))
     err = fail(NIC_EHIP, "host surface: range-word read-back failed");
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
     hipError_t e = host_wait(c->hev[2][k]);
@@ -1231,14 +1281,21 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   // (and the read-back's) means all three streams are idle -- no stream synchronisations
   // (~10-30 us per call); any error path drains them
   if (!err && issued == K && chain_check) {
-    const hipError_t e = host_wait(c->hev_caller);
+    hipError_t e = host_wait(c->hev_caller);
+    if (e == hipSuccess && two) e = host_wait(c->hev_alt);
     if (e != hipSuccess) err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
   }
   if (err || issued != K)
-    for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);
-  if (!err && chain_check && c->range_host[4]) {
+    for (int i = 0; i < 4; ++i) (void)hipStreamSynchronize(c->hs[i]);
+  if (!err && chain_check && (c->range_host[4] || (two && c->alt_host[4]))) {
     HIP_TRY(hipDeviceSynchronize());
     err = chain_timeout_check(c, c->range_host, "host surface");
+    if (two && c->alt_host[4]) {
+      swap_slot(c);
+      const int e2 = chain_timeout_check(c, c->alt_host, "host surface");
+      swap_slot(c);
+      if (!err) err = e2;
+    }
   }
   return err;
 }
@@ -1555,10 +1612,18 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   if (!c || !passes) return fail(NIC_EINVAL, "nic_range_trips: NULL argument");
   DeviceGuard guard(c->device);
   HIP_TRY(hipDeviceSynchronize());
-  int words[5] = {};
+  int words[5] = {}, alt[5] = {};
   HIP_TRY(hipMemcpy(words, c->range, sizeof(words), hipMemcpyDeviceToHost));
-  *passes = (int64_t)words[1] + c->error_trips;
-  return chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
+  if (c->alt.range) HIP_TRY(hipMemcpy(alt, c->alt.range, sizeof(alt), hipMemcpyDeviceToHost));
+  *passes = (int64_t)words[1] + alt[1] + c->error_trips;
+  int rc = chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
+  if (alt[4]) {  // the host pipeline's second slot
+    swap_slot(c);
+    const int rc2 = chain_timeout_check(c, alt, "nic_range_trips");
+    swap_slot(c);
+    if (!rc) rc = rc2;
+  }
+  return rc;
 }
 
 int nic_rerun_launch_info(nic_ctx* c, int* blocks_per_cu, int* grid, int* cooperative) {

@@ -3326,8 +3326,9 @@ bool k3pair_supported(int H, int W) {
 }
 
 // ------------------------------------------------------------------------------------
-// Fused k3 residual pair on Winograd F(2,3) along y (round 4; the default for planes up to
-// 64 columns; NIC_K3P=d keeps the direct pair above).  conv3 -> conv4 -> + x and
+// Fused k3 residual pair on Winograd F(2,3) along y (round 4; NIC_K3P=w, planes up to 64
+// columns; measured slower than the direct pair above, which stays the default: 0.304 vs
+// 0.261 ms, one wave per SIMD leaves the transform VALU unhidden -- DESIGN section 5b).  conv3 -> conv4 -> + x and
 // dconv5 -> dconv6 -> + x (encoder.py:22-25, decoder.py:26-29) with every conv computed two
 // output rows at a time:
 //   rows d0..d3 = in[y-1 .. y+2] of a pair (y, y+1):  V0 = d0 - d2, V1 = d1 + d2,

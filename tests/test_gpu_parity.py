@@ -364,6 +364,27 @@ def test_pack_unpack_bit_exact(codecs):
     np.testing.assert_array_equal(c.unpack(p).cpu().numpy(), z)
 
 
+def test_numpy_surface_concurrent_chunks(weights_spread):
+    """The host pipeline runs odd chunks on a second compute stream with the ctx's second pass
+    slot (own activation regions and range-guard words), so two chunk passes overlap: a config-2
+    batch (64 x 256^2) and ragged chunkings give the device path's bytes exactly."""
+    from neural_network_image_compression_amd.codec import Codec, Decoder, Encoder
+    c = Codec(0)
+    c.set_weights(weights_spread)
+    x = torch.randint(0, 256, (64, 256, 256, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(8))
+    zd = c.encode(x.cuda())
+    rd = c.decode(zd).cpu().numpy()
+    zd = zd.cpu().numpy()
+    enc, dec = Encoder(codec=c), Decoder(codec=c)
+    xh = x.numpy()
+    for chunks in (3, 2, 5, 16):
+        enc.host_chunks = dec.host_chunks = chunks
+        z = enc(xh)
+        assert np.array_equal(z, zd), chunks
+        assert np.array_equal(dec(z), rd), chunks
+    assert c.range_trips() == 0
+
+
 def test_numpy_surface_matches_device(codecs, golden, weights_spread):
     from neural_network_image_compression_amd.codec import Decoder, Encoder
     g = golden("imagenet4")
