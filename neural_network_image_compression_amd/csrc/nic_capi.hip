@@ -1149,11 +1149,14 @@ class CopyPool {
   std::condition_variable cv_;
 };
 
-// NIC_HOST_SLOTS=1 (A/B): every chunk pass on one compute stream and one pass slot
+// NIC_HOST_SLOTS=2 (A/B): odd chunks on a second compute stream with the second pass slot.
+// Not the default: measured slower (round trip 2.15-2.20 vs 1.93-1.96 ms, decode 1.21 vs 1.06
+// ms, profiles/r4_ab_logs.txt) -- two chunk passes' persistent kernels (one block per CU each)
+// contend for the CUs instead of filling each other's tails.
 bool host_two_slots() {
   static const bool on = [] {
     const char* e = getenv("NIC_HOST_SLOTS");
-    return !(e && e[0] == '1');
+    return e && e[0] == '2';
   }();
   return on;
 }
@@ -1220,8 +1223,7 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   std::vector<int> lo;
   host_chunk_plan(n, chunks, lo);
   const int K = (int)lo.size() - 1;
-  // odd chunks on the second compute stream with the second pass slot: a chunk's kernels fill
-  // the tails of the previous chunk's (one stream serialised them: ~0.1 ms per call at config 2)
+  // NIC_HOST_SLOTS=2: odd chunks on the second compute stream with the second pass slot
   const bool two = host_two_slots() && K > 1;
   hipStream_t cs[2] = {c->hs[1], two ? c->hs[3] : c->hs[1]};
   HIP_TRY(hipEventRecord(c->hev_caller, caller));

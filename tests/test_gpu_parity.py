@@ -364,10 +364,27 @@ def test_pack_unpack_bit_exact(codecs):
     np.testing.assert_array_equal(c.unpack(p).cpu().numpy(), z)
 
 
-def test_numpy_surface_concurrent_chunks(weights_spread):
-    """The host pipeline runs odd chunks on a second compute stream with the ctx's second pass
-    slot (own activation regions and range-guard words), so two chunk passes overlap: a config-2
-    batch (64 x 256^2) and ragged chunkings give the device path's bytes exactly."""
+@pytest.mark.parametrize("slots", ["1", "2"])
+def test_numpy_surface_concurrent_chunks(slots, weights_spread, tmp_path):
+    """The host pipeline on a config-2 batch (64 x 256^2) with ragged chunkings gives the device
+    path's bytes exactly -- with one compute stream (default) and with NIC_HOST_SLOTS=2 (odd
+    chunks on a second stream with the ctx's second pass slot: own activation regions and
+    range-guard words, two chunk passes in flight; child process, read at library load)."""
+    if slots == "2":
+        import subprocess
+        code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import torch; "
+                "import test_gpu_parity as T; "
+                "from neural_network_image_compression_amd import weights as W; "
+                "T._surface_check(W.seeded_weights(0, init='spread')); print('SLOTS-OK')"
+                % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__))))
+        out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, NIC_HOST_SLOTS="2"),
+                             capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0 and "SLOTS-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+        return
+    _surface_check(weights_spread)
+
+
+def _surface_check(weights_spread):
     from neural_network_image_compression_amd.codec import Codec, Decoder, Encoder
     c = Codec(0)
     c.set_weights(weights_spread)
@@ -466,12 +483,14 @@ def test_f16_range_guard(golden, weights_spread):
     range_guard_contract(golden, weights_spread)
 
 
-@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "1"}], ids=["per-layer", "cooperative"])
+@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "1"}, {"NIC_HOST_SLOTS": "2"}],
+                         ids=["per-layer", "cooperative", "host-two-slots"])
 def test_f16_range_guard_rerun_variants(switches):
     """The same contract with the gated re-run as one launch per layer (NIC_CHAIN=0: every
-    fp32 kernel checks the gate itself) and as a cooperative chained launch (NIC_COOP=1; the
-    default is a plain launch, see launch_fp32_chain); child process, the switches are read
-    when libnic.so loads."""
+    fp32 kernel checks the gate itself), as a cooperative chained launch (NIC_COOP=1; the
+    default is a plain launch, see launch_fp32_chain), and with the host surface's odd chunks
+    on the second pass slot (NIC_HOST_SLOTS=2: their trips land in its own guard words, summed
+    by nic_range_trips); child process, the switches are read when libnic.so loads."""
     import os
     import subprocess
     import sys
