@@ -2166,6 +2166,13 @@ constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in
 #ifndef NIC_C12_PT0
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
+#ifndef NIC_C12_U0
+// conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile) instead of whole
+// pixel tiles: each ts 0 wave takes NIC_C12_U0 units, the ts 1 waves the rest (0: whole tiles,
+// NIC_C12_PT0).  Whole tiles left the ts 0 chain 7,843 cycles per tile against the ts 1 chain's
+// 6,664 (profiles/r4n_c12_stamps.txt); a unit is ~550 cycles.
+#define NIC_C12_U0 5
+#endif
 
 // Padded colour planes of the fused conv1 (ConvArgs::cplane): origin offsets and sizes in
 // f16 elements for conv2's tile grid, so that tile (ty, tx)'s patch starts at row 32 ty,
@@ -2278,6 +2285,10 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     }
   }
   const float scale1 = a.wscale1[model];
+  // NIC_C12_U0: a wave's units (base + cg + 4k) all have channel tile (base + cg) & 1
+  const int uct = (TS == 0 ? cg : 20 + cg) & 1;
+  const f16x8 A1u_hi = uct ? A1[1][0] : A1[0][0], A1u_lo = uct ? A1[1][1] : A1[0][1];
+  const f32x4 b1u = uct ? b1[1] : b1[0];
   int poff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -2321,7 +2332,59 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     constexpr int NPT = (G::HH * G::HW + 15) / 16, PT0 = NIC_C12_PT0, PT1 = (NPT - 4 * PT0 + 3) / 4;
     static_assert(PT0 >= 0 && PT1 >= 0 && 4 * (PT0 + PT1) >= NPT, "conv1 shares cover the halo");
     constexpr int PTW = TS == 0 ? PT0 : PT1, PTB = TS == 0 ? 0 : 4 * PT0;
-    if constexpr (PTW > 0) {
+    // half-tile units: unit v = (pixel tile v >> 1, channel tile v & 1); this wave's units
+    // UB + cg + 4k, k < UW (all of channel tile uct)
+    constexpr int NU = 2 * NPT, U0 = NIC_C12_U0, U1 = (NU - 4 * U0 + 3) / 4;
+    constexpr int UW = TS == 0 ? U0 : U1, UB = TS == 0 ? 0 : 4 * U0;
+    static_assert(U0 >= 0 && U1 >= 0 && 4 * (U0 + U1) >= NU, "conv1 unit shares cover the halo");
+    if constexpr (NIC_C12_U0 > 0 && UW > 0) {
+      int p, t0y, t0x;
+      tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
+      char* halo = lds + (i & 1) * G::HALO_BYTES;
+      const char* ph = patches + (i & 1) * 2 * C12_PLANE;
+      const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;
+      f16x8 bh[UW], bl[UW];
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {
+        const int q = 16 * ((UB + cg + 4 * u) >> 1) + l16;
+        const int qq = q < G::HH * G::HW ? q : 0;
+        const int hy = qq / G::HW, hx = qq - hy * G::HW;
+        const char* pb = ph + (2 * hy * C12_PPW + hx) * 4;
+        u32x4 H, L;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          H[j] = *(const uint32_t*)(pb + poff[j]);
+          L[j] = *(const uint32_t*)(pb + C12_PLANE + poff[j]);
+        }
+        bh[u] = __builtin_bit_cast(f16x8, H);
+        bl[u] = __builtin_bit_cast(f16x8, L);
+      }
+      f32x4 c1[UW];
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {  // the same MFMA chain as the whole-tile form, per channel tile
+        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_lo, bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_hi, bl[u], c1[u], 0, 0, 0);
+        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_hi, bh[u], c1[u], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {
+        const int v = UB + cg + 4 * u;
+        if (v >= NU) break;  // wave-uniform
+        const int q = 16 * (v >> 1) + l16;
+        const bool qv = q < G::HH * G::HW;
+        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
+        const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
+        f32x4 vv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vv[r] = in1 ? leaky02(scale_bias(c1[u][r], scale1, b1u[r])) : 0.f;
+        range_track(rmax, vv);
+        f16x4 hi, lo;
+        split4(vv, hi, lo);
+        const u32x4 q16 = swap16_pair(hi, lo);
+        if (qv)
+          *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * uct + 4 * (g & ~1)) * 2) = q16;
+      }
+    } else if constexpr (NIC_C12_U0 == 0 && PTW > 0) {
       int p, t0y, t0x;
       tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
       char* halo = lds + (i & 1) * G::HALO_BYTES;
