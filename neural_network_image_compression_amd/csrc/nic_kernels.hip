@@ -2167,11 +2167,14 @@ constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
 #ifndef NIC_C12_U0
-// conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile) instead of whole
-// pixel tiles: each ts 0 wave takes NIC_C12_U0 units, the ts 1 waves the rest (0: whole tiles,
-// NIC_C12_PT0).  Whole tiles left the ts 0 chain 7,843 cycles per tile against the ts 1 chain's
-// 6,664 (profiles/r4n_c12_stamps.txt); a unit is ~550 cycles.
-#define NIC_C12_U0 5
+// A/B build (> 0): conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile)
+// instead of whole pixel tiles, NIC_C12_U0 units per ts 0 wave, the ts 1 waves the rest -- to
+// even out the ts 0 chain (7,843 cycles per tile) and the ts 1 chain (6,664,
+// profiles/r4n_c12_stamps.txt).  Measured slower: conv12 0.264-0.269 vs 0.237-0.243 ms, 4K 4.17 vs
+// 3.74 ms (profiles/r4_ab_logs.txt): every unit re-reads its pixel tile's im2col fragments
+// (8 ds_read_b32, 2-way conflicted) and runs one 3-MFMA chain instead of two, so a unit costs far
+// more than half a tile.  0: whole pixel tiles (NIC_C12_PT0).
+#define NIC_C12_U0 0
 #endif
 
 // Padded colour planes of the fused conv1 (ConvArgs::cplane): origin offsets and sizes in
