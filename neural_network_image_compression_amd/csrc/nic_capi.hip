@@ -317,8 +317,11 @@ struct nic_ctx {
   size_t ws_bytes = 0;
   uint32_t* counts = nullptr;
   size_t counts_bytes = 0;
-  // set only inside nic_encode_entropy: conv8's folded-histogram partial counts
+  // set only inside nic_encode_entropy: conv8's folded-histogram counts (fold_acc, [3n][256],
+  // zero between calls: the reduce clears what it reads)
   uint32_t* fold_part = nullptr;
+  uint32_t* fold_acc = nullptr;
+  size_t fold_acc_bytes = 0;
   char* qs = nullptr;  // MS-SSIM scratch (pooled scales + tile sums), grown on demand
   size_t qs_bytes = 0;
   // optional per-layer HIP-event timing (nic_set_timing): one event pair per layer and
@@ -596,6 +599,7 @@ int nic_destroy(nic_ctx* c) {
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
+  if (c->fold_acc) (void)hipFree(c->fold_acc);
   if (c->qs) (void)hipFree(c->qs);
   if (c->zero16) (void)hipFree(c->zero16);
   if (c->wproj) (void)hipFree(c->wproj);
@@ -1082,7 +1086,10 @@ int grow_pinned(uint8_t*& p, size_t& have, size_t need) {
 // delayed their copy-in past the previous chunk's pass.  Workers spin briefly after each copy
 // (the chunks of one call come ~0.1 ms apart), then sleep on a condition variable; the pool is
 // never destroyed (detached threads parked at exit).  NIC_HOST_COPY_THREADS: worker count
-// (default 7, plus the calling thread; 0 = plain memcpy).
+// (plus the calling thread).  Default 0 = plain memcpy on the calling thread: with 7 workers the
+// host-plan sweep measured the encoder 0.942 -> 0.865 ms on one box, but the bench's host path
+// swung between 1,809 and 2,160 MP/s with it against 2,084-2,213 without (profiles/r4_ab_logs.txt):
+// a worker descheduled under the box's CPU quota stalls the caller, which waits for every part.
 class CopyPool {
  public:
   static CopyPool& get() {
@@ -1113,7 +1120,7 @@ class CopyPool {
   static constexpr int kSpin = 1 << 15;
   CopyPool() {
     const char* e = getenv("NIC_HOST_COPY_THREADS");
-    nw_ = std::max(0, std::min(31, e ? atoi(e) : 7));
+    nw_ = std::max(0, std::min(31, e ? atoi(e) : 0));
     for (int i = 0; i < nw_; ++i) std::thread([this, i] { worker(i + 1); }).detach();
   }
   void part(int id) {  // 4 KB-aligned share id of nw_ + 1
@@ -1396,16 +1403,6 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
   return NIC_OK;
 }
 
-static int grow_counts(nic_ctx* c, size_t cb) {
-  if (cb <= c->counts_bytes) return NIC_OK;
-  if (c->counts) HIP_TRY(hipFree(c->counts));
-  c->counts = nullptr;
-  c->counts_bytes = 0;
-  HIP_TRY(hipMalloc(&c->counts, cb));
-  c->counts_bytes = cb;
-  return NIC_OK;
-}
-
 int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
                        float* bits, void* stream) {
   if (!c) return fail(NIC_EINVAL, "nic_encode_entropy: NULL ctx");
@@ -1429,18 +1426,28 @@ int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint
     if (rc || (!counts && !bits)) return rc;
     return nic_entropy_hist(c, latent, n, h8, w8, counts, bits, stream);
   }
-  int rc = grow_counts(c, hist_fold_scratch_bytes(n, h8, w8));
-  if (rc) return rc;
-  c->fold_part = c->counts;  // [blocks][2 n planes][256] (hist_fold_scratch_bytes)
-  rc = guarded(c, st, "nic_encode_entropy", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
+  const size_t fb = hist_fold_scratch_bytes(n, h8, w8);
+  if (fb > c->fold_acc_bytes) {  // zeroed once; every reduce clears what it read
+    if (c->fold_acc) HIP_TRY(hipFree(c->fold_acc));
+    c->fold_acc = nullptr;
+    c->fold_acc_bytes = 0;
+    HIP_TRY(hipMalloc(&c->fold_acc, fb));
+    HIP_TRY(hipMemset(c->fold_acc, 0, fb));
+    c->fold_acc_bytes = fb;
+  }
+  c->fold_part = c->fold_acc;
+  int rc = guarded(c, st, "nic_encode_entropy", fits, [&](bool x3, const RangeGuard& rg, bool timed) {
     return encode_pass(c, rgb, n, h, w, latent, nullptr, st, x3, rg, timed);
   });
   c->fold_part = nullptr;
-  if (rc) return rc;
+  if (rc) {  // conv8 may have counted: leave the accumulator clean for the next call
+    (void)hipMemsetAsync(c->fold_acc, 0, fb, st);
+    return rc;
+  }
   RangeGuard trip{};  // the split pass's epoch: a trip means the re-run rewrote the latent
   trip.flag = c->range;
   trip.epoch = c->epoch;
-  HIP_TRY(launch_hist_fold(c->counts, latent, n, h8, w8, trip, counts, bits, st));
+  HIP_TRY(launch_hist_fold(c->fold_acc, latent, n, h8, w8, trip, counts, bits, st));
   return NIC_OK;
 }
 

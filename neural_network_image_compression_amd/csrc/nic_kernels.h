@@ -60,7 +60,7 @@ struct ConvArgs {
   int ws_xcd;             // weight-stationary kernels: logical block = XCD-contiguous remap of blockIdx
   int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
   // conv8 (f16x3, OUT_U8_LATENT) with the latent histogram folded in (nic_encode_entropy):
-  // per block and plane of its group the partial counts [block][2 nimg][256]
+  // the counts [3 nimg][256], zero on entry, added to with device-scope atomics
   uint32_t* hist_part;
   int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
@@ -176,7 +176,7 @@ hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part,
 // tripped range guard -- the latent rewritten by the exact-fp32 re-run -- recounts from z)
 bool hist_fold_supported(int nimg, int h8, int w8);
 size_t hist_fold_scratch_bytes(int nimg, int h8, int w8);
-hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
+hipError_t launch_hist_fold(uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
                             uint32_t* counts, float* bits, hipStream_t st);
 hipError_t launch_pack(const uint8_t* src, uint8_t* dst, int nimg, int h8, int w8, bool unpack, hipStream_t st);
 

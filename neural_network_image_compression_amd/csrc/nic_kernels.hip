@@ -1722,7 +1722,6 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   int hcur = 0, hpend = -1;
   uint32_t hz = 0;
   int h1_p = 0, h1_y = 0, h1_x = 0, h2_p = 0, h2_y = 0, h2_x = 0;  // tiles i-1, i-2 (after tile_take)
-  const int hblk = blockIdx.x;  // partial row of this block (a group's blocks are contiguous)
   auto hist_flush = [&](int q) __attribute__((always_inline)) {  // both ts = 1 waves, 128 bins each
     uint32_t* hb = hist + (q & 1) * (256 * HIST_R);
     const int t = cg * 64 + lane;  // cg 0, 1 of the ts = 1 waves (NCG = 2)
@@ -1735,7 +1734,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         c += hb[bin * HIST_R + r];
         hb[bin * HIST_R + r] = 0;
       }
-      a.hist_part[((size_t)hblk * 2 * a.nimg + q) * 256 + bin] = c;
+      if (c) atomicAdd(a.hist_part + (size_t)(p0 + q) * 256 + bin, c);  // device scope, no return
     }
   };
   auto hist_close = [&] __attribute__((always_inline)) {  // this wave's code-0 count of hcur into bin 0
@@ -4895,46 +4894,36 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
 // blocks follow from the contiguous ranges).  If the split pass tripped the range guard, the
 // latent was rewritten by the exact-fp32 re-run after conv8 counted: the plane is recounted
 // from z (LDS atomics; the rare path).
-// 1024 threads per plane: 4 groups of 256 bins, each summing every 4th block's partial (8 loads
-// in flight per thread), met in LDS -- the plane's ~85-171 partials of 1 KB are read in a few
-// latency rounds instead of one after the other.
-__global__ __launch_bounds__(1024) void hist_fold_kernel(const uint32_t* __restrict__ part, int nimg, int per_plane,
-                                                         int by, int bc,
-                                                         const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
-                                                         float n_sym, uint32_t* __restrict__ counts,
-                                                         float* __restrict__ bits) {
-  __shared__ uint32_t h[4][256];
+// The folded histogram's reduce: conv8's blocks added their partial counts into acc (device-
+// scope atomics, one per non-zero bin per block and plane); one 256-thread block per plane
+// reads its 256 counts, clears them for the next call and computes the plane's entropy.
+// (Partial rows per block reduced here instead -- 85-171 x 1 KB per plane -- took 23 us, as
+// long as the two-call histogram.)  A tripped range guard: the latent was rewritten by the
+// exact-fp32 re-run after conv8 counted, so the plane is recounted from z.
+__global__ __launch_bounds__(256) void hist_fold_kernel(uint32_t* __restrict__ acc, int nimg,
+                                                        const uint8_t* __restrict__ z, int plane_px, RangeGuard trip,
+                                                        float n_sym, uint32_t* __restrict__ counts,
+                                                        float* __restrict__ bits) {
+  __shared__ uint32_t h[256];
   __shared__ double red[4];
-  const int p = blockIdx.x, bin = threadIdx.x & 255, grp = threadIdx.x >> 8;
+  const int p = blockIdx.x, bin = threadIdx.x;
   const bool tripped = trip.flag && *(volatile const int*)trip.flag == trip.epoch;
-  if (!tripped) {  // every block of the plane's group wrote its partial counts of the plane
-    const int gi = p < nimg ? 0 : 1, nb = gi ? bc : by, base = gi ? by : 0, q = p - (gi ? nimg : 0);
-    const uint32_t* src = part + ((size_t)base * 2 * nimg + q) * 256 + bin;
-    const size_t bstride = (size_t)2 * nimg * 256;
-    uint32_t acc[8] = {};
-    for (int b0 = grp; b0 < nb; b0 += 32) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = b0 + 4 * u;
-        if (b < nb) acc[u] += src[(size_t)b * bstride];
-      }
-    }
-    h[grp][bin] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  } else {
-    if (grp == 0) h[0][bin] = 0;
+  uint32_t c = acc[(size_t)p * 256 + bin];
+  acc[(size_t)p * 256 + bin] = 0u;  // ready for the next fold
+  if (tripped) {
+    h[bin] = 0;
     __syncthreads();
     const int n = p % nimg, type = p / nimg;
     const uint8_t* src = z + (size_t)n * plane_px * 96 + type * 32;
-    for (long long i = threadIdx.x; i < (long long)plane_px * 8; i += 1024) {
+    for (long long i = bin; i < (long long)plane_px * 8; i += 256) {
       const uint32_t w = *(const uint32_t*)(src + (i >> 3) * 96 + (i & 7) * 4);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) atomicAdd(&h[0][(w >> (8 * k)) & 255], 1u);
+      for (int k = 0; k < 4; ++k) atomicAdd(&h[(w >> (8 * k)) & 255], 1u);
     }
-    if (grp > 0) h[grp][bin] = 0;
+    __syncthreads();
+    c = h[bin];
   }
-  __syncthreads();
-  const uint32_t c = threadIdx.x < 256 ? (h[0][bin] + h[1][bin]) + (h[2][bin] + h[3][bin]) : 0u;
-  plane_entropy(c, threadIdx.x, p, n_sym, counts, bits, red);
+  plane_entropy(c, bin, p, n_sym, counts, bits, red);
 }
 
 __global__ __launch_bounds__(256) void pack_latent_kernel(const uint8_t* __restrict__ z, uint8_t* __restrict__ out,
@@ -5438,11 +5427,10 @@ bool hist_fold_supported(int nimg, int h8, int w8) {
   return 2LL * by <= pp && 2LL * bc <= pp;
 }
 
-size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {  // [block][2 nimg planes][256]
-  const long long pp = (long long)((h8 + 3) / 4) * ((w8 + 7) / 8);
-  int by, bc;
-  ws2_groups(nimg, pp, &by, &bc);
-  return (size_t)(by + bc) * 2 * nimg * 256 * sizeof(uint32_t);
+size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {  // the counts [3 nimg][256]
+  (void)h8;
+  (void)w8;
+  return (size_t)3 * nimg * 256 * sizeof(uint32_t);
 }
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
@@ -5763,13 +5751,10 @@ hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part,
   return hipGetLastError();
 }
 
-hipError_t launch_hist_fold(const uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
+hipError_t launch_hist_fold(uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,
                             uint32_t* counts, float* bits, hipStream_t st) {
   if (!hist_fold_supported(nimg, h8, w8)) return hipErrorInvalidValue;
-  const int pp = ((h8 + 3) / 4) * ((w8 + 7) / 8);
-  int by, bc;
-  ws2_groups(nimg, pp, &by, &bc);
-  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, nimg, pp, by, bc, z, h8 * w8, trip,
+  hipLaunchKernelGGL(hist_fold_kernel, dim3(3 * nimg), dim3(256), 0, st, part, nimg, z, h8 * w8, trip,
                      (float)h8 * w8 * 32.0f, counts, bits);
   return hipGetLastError();
 }
