@@ -3071,6 +3071,9 @@ __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_RE
 // columns (a.tiles_x of them); per strip the input rows carry 66 columns (2 each side), conv_a
 // computes 64 (the strip's 62 plus the column either side conv_b needs, zeros outside the
 // plane) and conv_b the strip's 62 (3 % of its lanes and 3 % of conv_a's work are the seams).
+#ifndef NIC_K3P_PRIO
+#define NIC_K3P_PRIO 1  // 0 (A/B build): both roles' MFMA streams at priority 1
+#endif
 template <int MT, bool SKEW, bool STRIP>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   constexpr int COUT = 64, KST = 2;
@@ -3183,7 +3186,12 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
       fb[m][0] = frag(m, 0, 0);
       fb[m][1] = frag(m, 0, 1);
     });
-    __builtin_amdgcn_s_setprio(1);
+    // NIC_K3P_PRIO: conv_b's stream (the role on the step's critical path by stamps: conv_a waits
+    // ~2,660 cycles per step at the barrier) outranks conv_a's when both have an MFMA ready
+    if (NIC_K3P_PRIO && role == 1)
+      __builtin_amdgcn_s_setprio(2);
+    else
+      __builtin_amdgcn_s_setprio(1);
     static_for<NSTEP>([&](auto stc) {
       constexpr int st = decltype(stc)::value, t = st / KST, ks = st % KST;
       static_for<MT>([&](auto mc) {
