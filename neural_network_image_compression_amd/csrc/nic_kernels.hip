@@ -2165,6 +2165,9 @@ constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in
 #ifndef NIC_C12_PT0
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
+#ifndef NIC_C12_PRIO
+#define NIC_C12_PRIO 1  // 0 (A/B build): both roles' conv2 streams at priority 1
+#endif
 #ifndef NIC_C12_U0
 // A/B build (> 0): conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile)
 // instead of whole pixel tiles, NIC_C12_U0 units per ts 0 wave, the ts 1 waves the rest -- to
@@ -2462,7 +2465,9 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
       fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
     }
-    __builtin_amdgcn_s_setprio(1);
+    // NIC_C12_PRIO: the ts 0 wave's conv2 stream (its chain is the tile period by stamps) outranks
+    // the ts 1 partner's when both have an MFMA ready
+    __builtin_amdgcn_s_setprio(NIC_C12_PRIO && TS == 0 ? 2 : 1);
     static_for<NG>([&](auto gqc) {
       constexpr int gq = decltype(gqc)::value;
       constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;

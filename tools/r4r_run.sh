@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
-  -k "golden or alternative or k3" > gpurun_out/r4r_tests.log 2>&1; rc=$?
+  -k "golden or alternative or k3 or encode" > gpurun_out/r4r_tests.log 2>&1; rc=$?
 echo "[tests] rc=$rc"; tail -3 gpurun_out/r4r_tests.log
 [ $rc -eq 0 ] || exit $rc
 B="--steps 30 --warmup 10 --no-cpu-baseline --no-parity --no-power-probe --no-host-path --no-quality"
@@ -18,5 +18,5 @@ import json
 for t in ("p1_1","p0_1","p1_2","p0_2","p1_3","p0_3"):
     d=json.loads(open(f"gpurun_out/r4r_{t}.json").read().strip().splitlines()[-1])
     L=d["layers"]
-    print(t, d["value"], d["ms_per_step"], {k: L[k].get("avg_ms") for k in ("conv4","dconv6","dconv7") if k in L})
+    print(t, d["value"], d["ms_per_step"], {k: L[k].get("avg_ms") for k in ("conv2","conv4","dconv6","dconv7") if k in L})
 PY
