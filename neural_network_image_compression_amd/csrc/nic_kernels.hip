@@ -2166,7 +2166,9 @@ constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
 #ifndef NIC_C12_PRIO
-#define NIC_C12_PRIO 1  // 0 (A/B build): both roles' conv2 streams at priority 1
+// ts 0's conv2 stream at priority 2 over ts 1's: conv12 0.2433-0.2441 vs 0.2446-0.2459 ms (3
+// alternating rounds, profiles/r4_ab_logs.txt); 0 (A/B build): both at priority 1
+#define NIC_C12_PRIO 1
 #endif
 #ifndef NIC_C12_U0
 // A/B build (> 0): conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile)
@@ -3077,7 +3079,10 @@ __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_RE
 // computes 64 (the strip's 62 plus the column either side conv_b needs, zeros outside the
 // plane) and conv_b the strip's 62 (3 % of its lanes and 3 % of conv_a's work are the seams).
 #ifndef NIC_K3P_PRIO
-#define NIC_K3P_PRIO 1  // 0 (A/B build): both roles' MFMA streams at priority 1
+// 1 (A/B build): conv_b's MFMA stream at priority 2 over conv_a's.  Measured slower: conv4 /
+// dconv6 0.261-0.264 vs 0.258-0.260 ms (3 alternating rounds, profiles/r4_ab_logs.txt) -- conv_a's
+// stream then finishes later, and so does its epilogue writing the rows conv_b needs next step.
+#define NIC_K3P_PRIO 0
 #endif
 template <int MT, bool SKEW, bool STRIP>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
