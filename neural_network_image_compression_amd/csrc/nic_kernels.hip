@@ -1673,6 +1673,9 @@ constexpr int C12_PP = 52;
 // Measured against other forms (4K frames, conv8 alone 0.891-0.900 ms): counting in the ts = 0
 // epilogue lengthened the critical pair of waves, and walks that give a block fewer planes
 // (a contiguous range per block: 1.069 ms; per XCD: 0.952 ms) lose the strip locality.
+#ifndef NIC_WS2_PRIO
+#define NIC_WS2_PRIO 1  // 0 (A/B build): the tap-split streams at the default priority
+#endif
 constexpr int HIST_R = 2;
 constexpr int HIST_LDS = 2 * 256 * HIST_R * 4 + 2 * 2 * 2 * 64 * 4;  // + codes [2][NCG][MT][64] (conv8)
 __host__ __device__ inline void hist_xcd_range(int rel, int nb, long long ntot, long long* start, long long* len, int* nx,
@@ -2071,6 +2074,9 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
       fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
     }
+    // NIC_WS2_PRIO: the MFMA streams at priority 1, the last tap group's (7 taps in conv8, the
+    // most per SIMD pair; its partner ts 1 waits ~1,740 cycles per tile) at 2
+    if constexpr (NIC_WS2_PRIO) __builtin_amdgcn_s_setprio(TS == NTS - 1 ? 2 : 1);
     static_for<NG>([&](auto gqc) {
       constexpr int gq = decltype(gqc)::value;
       constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;
@@ -2084,6 +2090,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the stream order
     });
+    if constexpr (NIC_WS2_PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (TS > 0) {  // partial sums of tile i for the ts = 0 wave of this cg
       char* pp = part + (((i & 1) * (NTS - 1) + TS - 1) * NCG + cg) * PART + lane * 16;
 #pragma unroll
