@@ -2075,8 +2075,11 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
     }
     // NIC_WS2_PRIO: the MFMA streams at priority 1, the last tap group's (7 taps in conv8, the
-    // most per SIMD pair; its partner ts 1 waits ~1,740 cycles per tile) at 2
-    if constexpr (NIC_WS2_PRIO) __builtin_amdgcn_s_setprio(TS == NTS - 1 ? 2 : 1);
+    // most per SIMD pair; its partner ts 1 waits ~1,740 cycles per tile) at 2: conv8 0.0620-0.0624
+    // vs 0.0637-0.0640 ms (3 alternating rounds, profiles/r4_ab_logs.txt).  Not with HIST: the
+    // ts 1 waves count the codes after their stream, and behind the priority that took conv8 on
+    // 4K frames from 0.925 to 1.047 ms.
+    if constexpr (NIC_WS2_PRIO && !HIST) __builtin_amdgcn_s_setprio(TS == NTS - 1 ? 2 : 1);
     static_for<NG>([&](auto gqc) {
       constexpr int gq = decltype(gqc)::value;
       constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;
@@ -2090,7 +2093,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the stream order
     });
-    if constexpr (NIC_WS2_PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (NIC_WS2_PRIO && !HIST) __builtin_amdgcn_s_setprio(0);
     if constexpr (TS > 0) {  // partial sums of tile i for the ts = 0 wave of this cg
       char* pp = part + (((i & 1) * (NTS - 1) + TS - 1) * NCG + cg) * PART + lane * 16;
 #pragma unroll
