@@ -3094,8 +3094,14 @@ __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_RE
 // stream then finishes later, and so does its epilogue writing the rows conv_b needs next step.
 #define NIC_K3P_PRIO 0
 #endif
+// Row ranges of the pair's blocks balanced by pipeline steps (launch_k3pair_x3): block b takes
+// rows [start[b], start[b + 1]) of the stream; start[0] < 0: the plain equal-rows split
+constexpr int K3P_MAX_GRID = 320;
+struct K3Ranges {
+  int start[K3P_MAX_GRID + 1];
+};
 template <int MT, bool SKEW, bool STRIP>
-__global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
+__global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a, K3Ranges rng) {
   constexpr int COUT = 64, KST = 2;
   __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
   char* in_ring = lds;
@@ -3110,8 +3116,15 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a) {
   static_assert(!STRIP || MT == 4, "strips are 4 M tiles wide");
   const int nstrips = STRIP ? a.tiles_x : 1;
   const long long total_rows = (long long)a.P * nstrips * H;
-  const long long per_block = (total_rows + gridDim.x - 1) / gridDim.x;
-  const long long g0 = (long long)blockIdx.x * per_block, g1 = min(g0 + per_block, total_rows);
+  long long g0, g1;
+  if (rng.start[0] >= 0) {
+    g0 = rng.start[blockIdx.x];
+    g1 = rng.start[blockIdx.x + 1];
+  } else {
+    const long long per_block = (total_rows + gridDim.x - 1) / gridDim.x;
+    g0 = (long long)blockIdx.x * per_block;
+    g1 = min(g0 + per_block, total_rows);
+  }
   const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
 
   // zero records: columns -1 and W.. of every ring row (never written afterwards)
@@ -5382,6 +5395,52 @@ hipError_t launch_k3wino_x3(const ConvArgs& a0, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Block row ranges of the fused pair by pipeline steps.  A block pays ~3 fill steps per segment
+// (the part of its range inside one (plane, strip) column of H rows) on top of one step per row:
+// equal-row ranges give the blocks that straddle a plane boundary 2 segments (config 2: 48 rows
+// = 54 steps against 51 for a one-segment block).  Greedy ranges under a step budget T, the
+// smallest T that fits the grid (binary search), even that out.  NIC_K3P_BAL = the per-segment
+// cost in steps (default 3; 0: the equal-rows split).
+static void k3pair_balance(long long total, int H, int G, K3Ranges& r) {
+  static const int F = [] {
+    const char* e = getenv("NIC_K3P_BAL");
+    const int v = e ? atoi(e) : 3;
+    return v >= 0 && v <= 64 ? v : 3;
+  }();
+  if (F == 0 || G <= 0 || G > K3P_MAX_GRID || total >= (1LL << 31) || H <= 0) return;
+  // blocks the greedy needs under budget T (stops counting past G); fills r when `write`
+  auto fill = [&](long long T, bool write) {
+    long long s = 0;
+    int b = 0;
+    while (s < total) {
+      if (b == G) return G + 1;
+      if (write) r.start[b] = (int)s;
+      ++b;
+      long long budget = T;
+      while (s < total && budget > F) {
+        const long long left = H - s % H, take = std::min(left, budget - F);
+        s += take;
+        budget -= take + F;
+        if (take < left) break;
+      }
+    }
+    if (write)
+      for (int k = b; k <= G; ++k) r.start[k] = (int)total;
+    return b;
+  };
+  const long long per = (total + G - 1) / G;
+  long long lo = F + 1, hi = per + F * (per / H + 2);  // the equal split fits hi
+  if (fill(hi, false) > G) return;
+  while (lo < hi) {
+    const long long mid = (lo + hi) / 2;
+    if (fill(mid, false) <= G)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  fill(hi, true);
+}
+
 hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (!k3pair_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wx2 || !a.bias2 || a.P != 3 * a.nimg)
@@ -5406,7 +5465,10 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
     const char* e = getenv("NIC_K3P_SK");
     return !(e && e[0] == '0');
   }();
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a); };
+  K3Ranges rng;
+  rng.start[0] = -1;
+  k3pair_balance(rows, a.H, grid, rng);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a, rng); };
   auto pick = [&](auto skc) {
     constexpr bool SK = decltype(skc)::value;
     if (a.tiles_x > 1) {

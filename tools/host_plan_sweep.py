@@ -38,6 +38,9 @@ SETTINGS = [("3", {}), ("3", {"NIC_HOST_COPY_THREADS": "0"}), ("3", {"NIC_HOST_E
             ("3", {"NIC_HOST_EDGE": "350"}), ("4", {"NIC_HOST_EDGE": "300"}), ("4", {}), ("2", {}),
             ("5", {"NIC_HOST_EDGE": "300"})]
 
+if len(sys.argv) > 1 and sys.argv[1] == "k3bal":  # step-balanced k3 pair ranges vs equal rows, 3 alternating rounds
+    SETTINGS = [("3", {}), ("3", {"NIC_K3P_BAL": "0"})] * 3
+    sys.argv[1:] = []
 for chunks, env in SETTINGS[:int(sys.argv[1]) if len(sys.argv) > 1 else None]:
     e = dict(os.environ, **env)
     out = subprocess.run([sys.executable, "-c", CHILD, chunks], env=e, capture_output=True, text=True, timeout=240)
