@@ -5400,12 +5400,13 @@ hipError_t launch_k3wino_x3(const ConvArgs& a0, hipStream_t st) {
 // equal-row ranges give the blocks that straddle a plane boundary 2 segments (config 2: 48 rows
 // = 54 steps against 51 for a one-segment block).  Greedy ranges under a step budget T, the
 // smallest T that fits the grid (binary search), even that out.  NIC_K3P_BAL = the per-segment
-// cost in steps (default 3; 0: the equal-rows split).
+// cost the budget charges, in steps (default 2: pair 0.2379-0.2385 ms vs 0.2388-0.2402 at 3,
+// 0.2392-0.2404 at 4 and 0.2415-0.2423 for the equal-rows split, NIC_K3P_BAL=0; same box).
 static void k3pair_balance(long long total, int H, int G, K3Ranges& r) {
   static const int F = [] {
     const char* e = getenv("NIC_K3P_BAL");
-    const int v = e ? atoi(e) : 3;
-    return v >= 0 && v <= 64 ? v : 3;
+    const int v = e ? atoi(e) : 2;
+    return v >= 0 && v <= 64 ? v : 2;
   }();
   if (F == 0 || G <= 0 || G > K3P_MAX_GRID || total >= (1LL << 31) || H <= 0) return;
   // blocks the greedy needs under budget T (stops counting past G); fills r when `write`
