@@ -7,7 +7,8 @@
 A step = nic_encode + nic_decode of one batch of `--batch` synthetic u8 256x256x3 images
 already resident in HBM (BASELINE config 2 at N=1; config 3's 8 x 64 sharding at N=8:
 weak scaling, each rank owns its own 64 images, no data-path collective).  Weights are
-the seeded 'spread' init (no trained checkpoint exists), generated on rank 0 and
+the seeded 'spread' init (random-init weights of the architecture; the trained codecs under
+tests/golden/trained are parity fixtures, not the timed workload), generated on rank 0 and
 broadcast over RCCL once at setup.
 
 Rank 0 prints ONE JSON line with the driver's keys plus:
@@ -584,7 +585,7 @@ def main():
                                 "4k": f"config5: {B}x{H}x{W}x3 frames per GPU, encode + histogram entropy"
                                 }[args.workload] + " (torch seed 1000+rank)",
                    "global_batch": world * B, "image": [H, W, 3], "parallelism": f"dp{world}",
-                   "weights": "seeded spread init (no trained checkpoint exists)"},
+                   "weights": "seeded spread init (random-init weights of the architecture)"},
         "step_tflops": round(total_flop / (ms_step * 1e-3) / 1e12, 2),
         "step_frac_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / peak, 4),
         "roofline": roofline, "layers": layers,
