@@ -216,6 +216,18 @@ def parity_sample(codec, x0, weights):
     return out
 
 
+def bench_weights(kind: str):
+    """The timed workload's weights: the seeded 'spread' init (default), or the committed
+    round-4 trained codec (entropy_loss_coef 0.01) for the informational operand comparison."""
+    from neural_network_image_compression_amd import weights as Wm
+    if kind == "seeded":
+        return Wm.seeded_weights(0)
+    pre = os.path.join(ROOT, "tests", "golden", "trained", "coef0.01_")
+    w = Wm.load(pre + "encoder", "encoder")
+    w.update(Wm.load(pre + "decoder", "decoder"))
+    return w
+
+
 def _free_port() -> int:
     import socket
 
@@ -290,6 +302,11 @@ def main():
                          "whole images encode+decode (config 4 shape); 4k: 3840x2160 frames, "
                          "encode + per-plane histogram entropy (config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--weights", default="seeded", choices=["seeded", "trained"],
+                    help="trained: the round-4 codec (entropy_loss_coef 0.01, tests/golden/trained) -- "
+                         "informational: the MFMA operands set the power-limited clock")
+    ap.add_argument("--images", default="random", choices=["random", "natural"],
+                    help="natural (config2 only): random 256x256 crops of kodim21 (tests/golden) -- informational")
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="arithmetic of the Cin>=32 convolutions (see include/nic.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -331,9 +348,9 @@ def main():
     if world > 1:
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
         from neural_network_image_compression_amd.parallel import broadcast_weights
-        weights = broadcast_weights(W.seeded_weights(0) if rank == 0 else None, dist)  # RCCL, once
+        weights = broadcast_weights(bench_weights(args.weights) if rank == 0 else None, dist)  # RCCL, once
     else:
-        weights = W.seeded_weights(0)
+        weights = bench_weights(args.weights)
 
     if args.workload == "config2":
         B, H, W = args.batch or 64, args.size, args.size
@@ -346,7 +363,14 @@ def main():
     codec.set_weights(weights)
     codec.reserve(B, H, W)
     g = torch.Generator().manual_seed(1000 + rank)
-    x = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8).to(device)
+    if args.images == "natural" and args.workload == "config2" and H <= 512 and W <= 768:
+        # SURVEY 8(d) config 2's natural-image variant: random crops of kodim21
+        k = torch.from_numpy(np.load(os.path.join(ROOT, "tests", "golden", "kodim21_full.npz"))["x"][0])
+        ys = torch.randint(0, 512 - H + 1, (B,), generator=g).tolist()
+        xs = torch.randint(0, 768 - W + 1, (B,), generator=g).tolist()
+        x = torch.stack([k[y:y + H, c:c + W] for y, c in zip(ys, xs)]).contiguous().to(device)
+    else:
+        x = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8).to(device)
     from neural_network_image_compression_amd._lib import latent_shape
     h8, w8 = latent_shape(H, W)
     z = torch.empty((B, h8, w8, 96), dtype=torch.uint8, device=device)
@@ -579,13 +603,14 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32" if args.precision == "fp32" else "fp32 (split-f16x3 MFMA)",
-        "data": "synthetic",
+        "data": "synthetic" if args.images == "random" or args.workload != "config2" else "kodim21 crops",
         "config": {"workload": {"config2": f"config2: {B}x{H}x{W}x3 u8 synthetic per GPU, encode+decode",
                                 "kodak": f"config4 shape: {B}x{H}x{W}x3 whole images per GPU, encode+decode",
                                 "4k": f"config5: {B}x{H}x{W}x3 frames per GPU, encode + histogram entropy"
                                 }[args.workload] + " (torch seed 1000+rank)",
                    "global_batch": world * B, "image": [H, W, 3], "parallelism": f"dp{world}",
-                   "weights": "seeded spread init (random-init weights of the architecture)"},
+                   "weights": "seeded spread init (random-init weights of the architecture)" if args.weights == "seeded"
+                   else "trained codec, entropy_loss_coef 0.01 (tests/golden/trained)"},
         "step_tflops": round(total_flop / (ms_step * 1e-3) / 1e12, 2),
         "step_frac_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / peak, 4),
         "roofline": roofline, "layers": layers,
