@@ -1,7 +1,8 @@
 """Child-process parity check of the alternative f16x3 kernels: NIC_WS=0 selects the
 one-tile-per-block split-f16 convs (conv2..conv8, dconv5..dconv7) and the standalone conv1
 instead of the weight-stationary / fused ones; NIC_D8=tile / NIC_D8=strip run dconv8 as its
-own MFMA kernel (tile or strip walk) instead of dconv7's fused projection + gather.  The
+own MFMA kernel (tile or strip walk) instead of dconv7's fused projection + gather; NIC_K3P_BAL=0
+gives the fused k3 pair's blocks equal row ranges instead of step-balanced ones.  The
 switches are read once when libnic.so loads, so they cannot be toggled inside the pytest
 process.  Run by tests/test_gpu_parity.py::test_alternative_kernels_parity;
 applies the same contract as the golden encode/decode tests there and prints ALT-OK."""
@@ -27,6 +28,7 @@ def main():
     ws_off = os.environ.get("NIC_WS") == "0"
     assert (ws_off or os.environ.get("NIC_D8") in ("tile", "strip") or os.environ.get("NIC_D8G") == "l"
             or os.environ.get("NIC_K3P") in ("0", "w") or os.environ.get("NIC_K3P_SK") == "0"
+            or os.environ.get("NIC_K3P_BAL") == "0"
             or os.environ.get("NIC_D1") in ("x", "p"))
     c = Codec(0, precision="f16x3")
     c.set_weights(W.seeded_weights(0, init="spread"))
