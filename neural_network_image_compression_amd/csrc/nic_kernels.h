@@ -63,6 +63,7 @@ struct ConvArgs {
   // the counts [3 nimg][256], zero on entry, added to with device-scope atomics
   uint32_t* hist_part;
   int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
+  int d1_mixed;           // dconv1_all: one block group over both models' tiles (weights reloaded at the switch)
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
   const uint16_t* wx2;

@@ -2894,14 +2894,20 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cg = wave & 3;
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   const int per_plane = a.tiles_y * a.tiles_x;
-  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
+  // d1_mixed: one group walks both models' planes (Y first), the weights reloaded when a tile
+  // of the other model comes up -- 12 tiles for every block at config 2 instead of 13 for a few
+  // Y blocks (1,024 Y tiles cannot split evenly over 85 of 256 blocks)
+  const int p0 = a.d1_mixed ? 0 : model ? a.nimg : 0, np = a.d1_mixed ? a.P : model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
   const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
   if (ntile == 0) return;  // block-uniform
 
   f16x8 w1[NT1][2], w2[NT2][2];
-  {
-    const char* wsrc = (const char*)a.wx + (size_t)model * 25 * TAP_BYTES;
+  float scale;
+  f32x4 bias;
+  int cur = -1;  // model of the resident weights
+  auto load_weights = [&](int m) __attribute__((always_inline)) {
+    const char* wsrc = (const char*)a.wx + (size_t)m * 25 * TAP_BYTES;
     auto frag_w = [&](int tap, int hl) {
       return *(const f16x8*)(wsrc + (size_t)tap * TAP_BYTES + ((((g >> 1) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
     };
@@ -2913,9 +2919,11 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     for (int t = 0; t < NT2; ++t)
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) w2[t][hl] = frag_w(TB2 + t, hl);
-  }
-  const float scale = a.wscale[model] * 0.0039215688593685627f;  // 2^-k and the dequantiser's 1/255
-  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + cg * 16 + 4 * g);
+    scale = a.wscale[m] * 0.0039215688593685627f;  // 2^-k and the dequantiser's 1/255
+    bias = *(const f32x4*)(a.bias + m * COUT + cg * 16 + 4 * g);
+    cur = m;
+  };
+  if (!a.d1_mixed) load_weights(model);
 
   // code staging: thread q = threadIdx.x + 512 j loads dword q & 7 of halo pixel q >> 3
   int st_lds[D1A_LD], st_hy[D1A_LD], st_hx[D1A_LD];
@@ -3013,6 +3021,10 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     stage_barrier();  // tile i's halo complete; tile i-2's reads of this buffer done everywhere
     int pl, ty, tx;
     it_run.take(pl, ty, tx);
+    if (a.d1_mixed) {  // wave-uniform: the tile's model
+      const int m = p0 + pl >= a.nimg ? 1 : 0;
+      if (m != cur) load_weights(m);
+    }
     if constexpr (NIC_D1A_PF == 2) {
       if (i + 2 < ntile) load_codes(cq);  // tile i+2: lands during this tile's and the next's MFMAs
     } else {  // A/B build: one tile ahead
@@ -5731,7 +5743,14 @@ static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = by;
   a.ws_blk[2] = by + bc;
-  hipLaunchKernelGGL(dconv1_all_kernel, dim3(by + bc), dim3(512), 0, st, a);
+  // NIC_D1M=0: per-model block groups (A/B); default one group over both models' tiles
+  static const bool mixed = [] {
+    const char* e = getenv("NIC_D1M");
+    return !(e && e[0] == '0');
+  }();
+  a.d1_mixed = mixed ? 1 : 0;
+  if (mixed) a.ws_blk[1] = a.ws_blk[2] = (int)std::min<long long>(nt, target);  // one group: gi = 0, nb = grid
+  hipLaunchKernelGGL(dconv1_all_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   return hipGetLastError();
 }
 
