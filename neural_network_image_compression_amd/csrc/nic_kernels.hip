@@ -5743,10 +5743,12 @@ static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = by;
   a.ws_blk[2] = by + bc;
-  // NIC_D1M=0: per-model block groups (A/B); default one group over both models' tiles
+  // NIC_D1M=1: one block group over both models' tiles (every block 12 tiles at config 2
+  // instead of 13 for a few Y blocks) -- measured slower, the mid-walk weight reload costs more
+  // than the tail: dconv1 0.0604-0.0608 vs 0.0555-0.0567 ms (3 rounds, profiles/r4_ab_logs.txt)
   static const bool mixed = [] {
     const char* e = getenv("NIC_D1M");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   a.d1_mixed = mixed ? 1 : 0;
   if (mixed) a.ws_blk[1] = a.ws_blk[2] = (int)std::min<long long>(nt, target);  // one group: gi = 0, nb = grid

@@ -644,9 +644,9 @@ def _alt_child(tmp_path, switches, tag):
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
                                       {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}, {"NIC_K3P_BAL": "0"},
-                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}, {"NIC_D1M": "0"}],
+                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}, {"NIC_D1M": "1"}],
                          ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "k3-equal-rows",
-                              "dconv1-tile", "dconv1-perphase", "dconv1-model-groups"])
+                              "dconv1-tile", "dconv1-perphase", "dconv1-mixed-groups"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the k3 layers
@@ -655,11 +655,11 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     golden contract too; they run in a child process because the switches are read when the
     library loads."""
     dump = _alt_child(tmp_path, switches, "v")
-    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_D1M": "0"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
+    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_D1M": "1"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
                     {"NIC_K3P_BAL": "0"}):
         # the LDS-staged gather sums the same projections in the same order as the direct one;
         # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue, with
-        # one block group over both models or one group per model (NIC_D1M=0); the
+        # one block group per model or one over both models (NIC_D1M=1); the
         # default (direct 9-tap) fused k3 residual pair runs the same chains and epilogues as
         # the two weight-stationary launches, in either step order and under either block range
         # split (a range boundary inside a plane recomputes the same conv_a row): bit-identical
