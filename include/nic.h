@@ -93,7 +93,13 @@ enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
  *     and overwrite every output.  No host synchronisation; results always fp32-class.
  *   NIC_RANGE_ERROR -- the call synchronises its stream after the split pass and returns
  *     NIC_ERANGE if it tripped (outputs undefined).
- * nic_range_trips (synchronising) counts the passes that tripped since nic_create. */
+ * nic_range_trips (synchronising) counts the passes that tripped since nic_create.
+ * A FALLBACK re-run runs as one chained launch with a bounded grid barrier; should that barrier
+ * ever time out (blocks not co-resident), the ctx marks it and every later chained re-run on the
+ * ctx exits at entry -- so device-pointer FALLBACK calls of that window that trip return NIC_OK
+ * with the split pass's (undefined) outputs -- until the next synchronising call
+ * (nic_range_trips, an ERROR-policy call or a host-array call) reports NIC_EHIP once and
+ * clears the mark. */
 enum { NIC_RANGE_FALLBACK = 0, NIC_RANGE_ERROR = 1 };
 int nic_set_range_policy(nic_ctx* ctx, int policy);
 int nic_range_trips(nic_ctx* ctx, int64_t* passes);
@@ -174,6 +180,9 @@ int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8,
  * two calls. */
 int nic_encode_entropy(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
                        float* bits, void* stream);
+/* 1 in *folds when nic_encode_entropy on (n, h, w) images (counts or bits requested) takes the
+ * folded form on ctx's device and precision, 0 when it runs the two calls. */
+int nic_encode_entropy_fold(nic_ctx* ctx, int n, int h, int w, int* folds);
 
 /* MS-SSIM of tf.image.ssim_multiscale(a, b, max_val=255) (tf2_0/tests/calc_ssim.py:13)
  * per image: a, b u8 (n,h,w,3) -> ms_ssim (n,) fp32.  TF defaults: 11-tap Gaussian
@@ -197,8 +206,9 @@ int nic_sq_err(const uint8_t* a, const uint8_t* b, int n, int64_t bytes_per_imag
  *                   Pillow and this library link the same zlib 1.2.11 here).
  *   NIC_PNG_TF      tf.image.encode_png(compression=-1), what get_bpp sizes
  *                   (training.py:12-21): libpng 1.6 defaults -- the same filter heuristic,
- *                   zlib default level (6) / memLevel 8 / Z_FILTERED, libpng's window
- *                   reduction and CMF rewrite for small images, 8,192-B IDATs.  TensorFlow is
+ *                   zlib default level (6) / memLevel 9 (png_io sets MAX_MEM_LEVEL) /
+ *                   Z_FILTERED, libpng's window reduction and CMF rewrite for small images and
+ *                   its filter pruning for 1-row / 1-column images, 8,192-B IDATs.  TensorFlow is
  *                   not importable here: parity with its own output is UNPINNED.
  * nic_png_encode writes file i at out + i * out_stride (out_stride >= nic_png_bound; out may
  * be NULL for sizes only) and its byte count to sizes[i].  nic_png_sizes = the Pillow sizes

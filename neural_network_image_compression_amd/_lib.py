@@ -60,6 +60,8 @@ _SIGNATURES = {
     "nic_entropy_hist": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "nic_encode_entropy": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp,
                                           c_vp]),
+    "nic_encode_entropy_fold": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int)]),
     "nic_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "nic_get_precision": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),
     "nic_set_range_policy": (ctypes.c_int, [c_vp, ctypes.c_int]),

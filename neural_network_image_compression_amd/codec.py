@@ -181,6 +181,14 @@ class Codec:
         _lib.check(rc, "nic_encode_entropy")
         return (z, bits, cnt) if counts else (z, bits)
 
+    def encode_entropy_folds(self, n: int, h: int, w: int) -> bool:
+        """True when encode_entropy on (n, h, w) images counts the codes inside conv8 (the fold),
+        False when it runs encode + entropy (nic_encode_entropy_fold)."""
+        import ctypes
+        f = ctypes.c_int()
+        _lib.check(self._L.nic_encode_entropy_fold(self._h, n, h, w, ctypes.byref(f)), "nic_encode_entropy_fold")
+        return bool(f.value)
+
     def decode(self, z, rgb_f32: bool = False, out=None):
         """(N,h,w,96) u8 -> (N,8h,8w,3) u8 [, fp32 clipped RGB before quantisation]."""
         torch = _torch()

@@ -1403,6 +1403,22 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
   return NIC_OK;
 }
 
+// the fold needs the split-f16 pass with the tap-split conv8 and >= 2 of a plane's conv8 tiles
+// per block of its group (hist_fold_supported); otherwise nic_encode_entropy runs the two calls
+static bool encode_entropy_folds(const nic_ctx* c, int n, int h, int w) {
+  const EncGeom eg = enc_geom(n, h, w);
+  return c->precision == NIC_PRECISION_F16X3 && x3_plane_fits(eg.c2y.out, eg.c2x.out) && conv12_fused() &&
+         hist_fold_supported(n, eg.c8y.out, eg.c8x.out);
+}
+
+int nic_encode_entropy_fold(nic_ctx* c, int n, int h, int w, int* folds) {
+  if (!c || !folds) return fail(NIC_EINVAL, "nic_encode_entropy_fold: NULL argument");
+  if (n <= 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode_entropy_fold: bad input shape (%d,%d,%d,3)", n, h, w);
+  DeviceGuard guard(c->device);
+  *folds = encode_entropy_folds(c, n, h, w) ? 1 : 0;
+  return NIC_OK;
+}
+
 int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
                        float* bits, void* stream) {
   if (!c) return fail(NIC_EINVAL, "nic_encode_entropy: NULL ctx");
@@ -1419,8 +1435,7 @@ int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint
   const bool fits = x3_plane_fits(eg.c2y.out, eg.c2x.out);
   // the fold needs the split-f16 pass with the tap-split conv8 and block ranges within a plane;
   // otherwise (and for counts == bits == NULL) the two-step form
-  const bool fold = (counts || bits) && c->precision == NIC_PRECISION_F16X3 && fits && conv12_fused() &&
-                    hist_fold_supported(n, h8, w8);
+  const bool fold = (counts || bits) && encode_entropy_folds(c, n, h, w);
   if (!fold) {
     int rc = nic_encode(c, rgb, n, h, w, latent, nullptr, stream);
     if (rc || (!counts && !bits)) return rc;

@@ -172,9 +172,11 @@ size_t hist_scratch_bytes(int nimg, int plane_px);
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
                        hipStream_t st);
 // the histogram folded into conv8 (nic_encode_entropy): whether the split-f16 conv8 launch can
-// count for this shape (each block's contiguous tile range spans at most two planes), the
-// partial-count scratch it needs (ids follow the counts), and the reduce (counts / bits; a
-// tripped range guard -- the latent rewritten by the exact-fp32 re-run -- recounts from z)
+// count for this shape (each block's strided walk visits >= 2 tiles of every plane it touches:
+// blocks of a model group <= conv8 tiles per plane / 2), the [3 nimg][256] count accumulator
+// conv8's blocks add into with device-scope atomics (LDS histograms alternated by plane parity,
+// flushed one tile after the plane changes), and the reduce that reads + clears it (counts /
+// bits; a tripped range guard -- the latent rewritten by the exact-fp32 re-run -- recounts from z)
 bool hist_fold_supported(int nimg, int h8, int w8);
 size_t hist_fold_scratch_bytes(int nimg, int h8, int w8);
 hipError_t launch_hist_fold(uint32_t* part, const uint8_t* z, int nimg, int h8, int w8, RangeGuard trip,

@@ -4942,11 +4942,6 @@ __global__ __launch_bounds__(1024) void hist_entropy_kernel(const uint32_t* __re
   plane_entropy(c, bin, p, n_sym, counts, bits, red);
 }
 
-// The folded histogram's reduce (nic_encode_entropy): plane p sums the partial counts of the
-// conv8 blocks whose tile ranges meet it (plane ids stored beside the counts; the candidate
-// blocks follow from the contiguous ranges).  If the split pass tripped the range guard, the
-// latent was rewritten by the exact-fp32 re-run after conv8 counted: the plane is recounted
-// from z (LDS atomics; the rare path).
 // The folded histogram's reduce: conv8's blocks added their partial counts into acc (device-
 // scope atomics, one per non-zero bin per block and plane); one 256-thread block per plane
 // reads its 256 counts, clears them for the next call and computes the plane's entropy.

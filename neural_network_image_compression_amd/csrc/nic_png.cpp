@@ -18,12 +18,15 @@
 // NIC_PNG_TF -- tf.image.encode_png(compression=-1): TensorFlow's png_io WriteImageToBuffer
 // on libpng 1.6 defaults: the same adaptive filter choice (libpng's minimum-sum-of-absolute-
 // differences heuristic over all five filters, first on ties, zero row above the first),
-// deflate at zlib's default level (Z_DEFAULT_COMPRESSION = 6), memLevel 8, Z_FILTERED, the
+// deflate at zlib's default level (Z_DEFAULT_COMPRESSION = 6), memLevel 9 (png_io's
+// png_set_compression_mem_level(MAX_MEM_LEVEL) after the level), Z_FILTERED, the
 // window reduced for images under 16 KiB of filtered data (png_deflate_claim; the stream is
 // the same, only the zlib header's window field differs, which optimize_cmf rewrites as
 // libpng does), IDAT chunks of libpng's 8,192-byte zbuffer, no ancillary chunks.  TensorFlow
 // is not importable here, so this mode is a restatement of those libraries' published
-// behaviour: parity with TF's own output is unpinned.
+// behaviour: parity with TF's own output is unpinned.  libpng's png_write_start_row prunes the
+// candidate filters of degenerate images: one row drops Up, Average and Paeth, one pixel
+// column drops Sub, Average and Paeth (restated here in TF mode; Pillow tries all five).
 // Byte equality with Pillow also assumes the deflate Pillow links is the same algorithm as the
 // system zlib this library links (-lz): true for the image's Pillow (tests/test_png_encode.py
 // compares the files); a Pillow built on zlib-ng or libdeflate would choose other matches.
@@ -51,7 +54,7 @@ struct PngMode {
   int level, mem_level, idat;  // deflate level, memLevel, IDAT chunk size
   bool libpng;                 // window reduction + CMF rewrite of libpng (NIC_PNG_TF)
 };
-constexpr PngMode kModes[2] = {{9, 9, 65536, false}, {Z_DEFAULT_COMPRESSION, 8, 8192, true}};
+constexpr PngMode kModes[2] = {{9, 9, 65536, false}, {Z_DEFAULT_COMPRESSION, 9, 8192, true}};
 
 inline int paeth(int a, int b, int c) {
   const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
@@ -59,14 +62,17 @@ inline int paeth(int a, int b, int c) {
 }
 
 // filtered rows of one image of h rows of w bytes (bpp bytes per pixel) into out
-// ((w + 1) * h bytes); cand: 5 * w scratch; zeros: w zero bytes
-void filter_rows(const uint8_t* img, int h, int w, int bpp, uint8_t* out, uint8_t* cand, const uint8_t* zeros) {
+// ((w + 1) * h bytes); cand: 5 * w scratch; zeros: w zero bytes; allowed: bit f set = filter f
+// is a candidate (libpng's pruning in TF mode)
+void filter_rows(const uint8_t* img, int h, int w, int bpp, uint8_t* out, uint8_t* cand, const uint8_t* zeros,
+                 unsigned allowed) {
   const uint8_t* prev = zeros;  // the row above the first is zero
   for (int r = 0; r < h; ++r) {
     const uint8_t* x = img + (size_t)r * w;
     long best_sum = -1;
     int best = 0;
     for (int f = 0; f < 5; ++f) {
+      if (!((allowed >> f) & 1u)) continue;
       uint8_t* o = cand + (size_t)f * w;
       long sum = 0;
       for (int i = 0; i < w; ++i) {
@@ -232,12 +238,16 @@ extern "C" int nic_png_encode(const uint8_t* images, int m, int h, int w, int ch
     return nic::set_error(NIC_ESHAPE, "nic_png_encode: out_stride below nic_png_bound");
   const PngMode& md = kModes[mode];
   const int bpp = channels, wb = w * channels;  // bytes per pixel / per row
+  // libpng png_write_start_row (TF mode): None 0, Sub 1, Up 2, Average 3, Paeth 4
+  unsigned allowed = 0x1fu;
+  if (md.libpng && h == 1) allowed &= ~((1u << 2) | (1u << 3) | (1u << 4));
+  if (md.libpng && w == 1) allowed &= ~((1u << 1) | (1u << 3) | (1u << 4));
   const int nt = std::max(1, std::min(threads > 0 ? threads : 1, m));
   std::atomic<int> next{0}, failed{0};
   auto work = [&]() {
     std::vector<uint8_t> filt((size_t)h * (wb + 1)), cand((size_t)5 * wb), zeros((size_t)wb, 0), z;
     for (int i = next.fetch_add(1); i < m; i = next.fetch_add(1)) {
-      filter_rows(images + (size_t)i * h * wb, h, wb, bpp, filt.data(), cand.data(), zeros.data());
+      filter_rows(images + (size_t)i * h * wb, h, wb, bpp, filt.data(), cand.data(), zeros.data(), allowed);
       const long len = deflate_rows(filt.data(), filt.size(), md, z);
       if (len < 0) {
         failed.store(1);

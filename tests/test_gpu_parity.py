@@ -292,18 +292,43 @@ def test_encode_entropy_fold(shape, weights_spread, weights_trained):
 
 
 def test_encode_entropy_fold_after_range_trip(golden, weights_spread):
-    """A tripped split pass: the exact-fp32 re-run rewrites the latent after conv8 counted, so
-    the fold's reduce recounts from the new latent -- counts / bits equal the two-call form."""
+    """A tripped split pass on a shape where the fold applies (two 4K frames): the exact-fp32
+    re-run rewrites the latent after conv8 counted, so the fold's reduce recounts each plane from
+    the new latent -- counts / bits equal the two-call form on the re-run's latent.  Then the
+    ERROR policy: the tripped call fails, and the next clean call finds the accumulator cleared
+    (its counts equal the two-call form)."""
     from neural_network_image_compression_amd.codec import Codec
-    g = golden("kodim21_256")
+    n, h, w = 2, 2160, 3840
+    x = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(77)).cuda()
     c = Codec(0)
     c.set_weights(range_scaled_weights(weights_spread))
-    x = _dev(np.concatenate([g["x"]] * 4))
+    assert c.encode_entropy_folds(n, h, w)
+    assert not c.encode_entropy_folds(4, 256, 256)  # the two-call shape of the sibling tests
     z1, bits1, cnt1 = c.encode_entropy(x, counts=True)
     assert c.range_trips() == 1
     bits2, cnt2 = c.entropy(z1, counts=True)
     assert torch.equal(cnt1, cnt2) and torch.equal(bits1, bits2)
-    check_codes(z1[:1].cpu().numpy(), g["latent"], g["prequant"])
+    assert torch.equal(z1, c.encode(x))  # the re-run's latent is the plain encoder's
+    assert c.range_trips() == 2
+    # ERROR policy: the trip is reported; the accumulator conv8 counted into is cleared
+    from neural_network_image_compression_amd import _lib
+    c.set_range_policy("error")
+    with pytest.raises(_lib.NicError) as e:
+        c.encode_entropy(x, counts=True)
+    assert e.value.code == _lib.NIC_ERANGE
+    clean = Codec(0)
+    clean.set_weights(weights_spread)
+    c.set_weights(weights_spread)
+    z3, bits3, cnt3 = c.encode_entropy(x, counts=True)
+    z4, bits4, cnt4 = clean.encode_entropy(x, counts=True)
+    bits5, cnt5 = clean.entropy(z4, counts=True)
+    assert torch.equal(z3, z4) and torch.equal(cnt3, cnt5) and torch.equal(bits3, bits5)
+    assert torch.equal(cnt4, cnt5)
+    g = golden("kodim21_256")  # and the tripped two-call form still reproduces the golden codes
+    c2 = Codec(0)
+    c2.set_weights(range_scaled_weights(weights_spread))
+    z6 = c2.encode(_dev(g["x"]))
+    check_codes(z6.cpu().numpy(), g["latent"], g["prequant"])
 
 
 def test_entropy_large_and_edge_planes(codecs):

@@ -5,7 +5,7 @@
   reconstructions and greyscale planes, over multi-IDAT sizes and thread counts.
 * NIC_PNG_TF (tf.image.encode_png(compression=-1), what get_bpp sizes, training.py:12-21):
   TensorFlow is not importable here, so the mode is pinned against an independent Python
-  restatement of libpng 1.6's defaults (filter heuristic, zlib level 6 / memLevel 8 /
+  restatement of libpng 1.6's defaults (filter heuristic, zlib level 6 / memLevel 9 /
   Z_FILTERED / reduced window, 8,192-byte IDATs) built on the zlib module, and every file is
   decoded by Pillow back to the input pixels.  Parity with TF's own bytes stays unpinned.
 CPU only: host threads, no GPU."""
@@ -80,8 +80,15 @@ def test_save_imgs_writes_pillow_files(tmp_path):
 # --- NIC_PNG_TF: an independent restatement of libpng 1.6's writer defaults ----------------
 
 def _filter_libpng(img, bpp):
-    """png_write_find_filter: all five filters, least sum of min(v, 256 - v), first on ties."""
+    """png_write_find_filter: least sum of min(v, 256 - v), first on ties, over the filters
+    png_write_start_row leaves: all five, minus Up / Average / Paeth for a one-row image and
+    minus Sub / Average / Paeth for a one-pixel-wide one."""
     h, w = img.shape
+    allowed = {0, 1, 2, 3, 4}
+    if h == 1:
+        allowed -= {2, 3, 4}
+    if w == bpp:
+        allowed -= {1, 3, 4}
     prev = np.zeros(w, np.int32)
     rows = []
     for r in range(h):
@@ -95,6 +102,8 @@ def _filter_libpng(img, bpp):
         cands = [x, x - a, x - prev, x - ((a + prev) >> 1), x - paeth]
         best, best_sum = None, None
         for f, v in enumerate(cands):
+            if f not in allowed:
+                continue
             v = v & 255
             s = int(np.minimum(v, 256 - v).sum())
             if best_sum is None or s < best_sum:
@@ -114,7 +123,7 @@ def _tf_png_restated(img):
         while len(raw) + 262 <= half:
             half >>= 1
             wb -= 1
-    co = zlib.compressobj(6, zlib.DEFLATED, max(wb, 9), 8, zlib.Z_FILTERED)
+    co = zlib.compressobj(6, zlib.DEFLATED, max(wb, 9), 9, zlib.Z_FILTERED)  # png_io: MAX_MEM_LEVEL
     z = bytearray(co.compress(raw) + co.flush())
     if len(raw) <= 16384 and (z[0] & 0x0F) == 8 and (z[0] & 0xF0) <= 0x70:  # optimize_cmf
         cinfo = z[0] >> 4
@@ -146,7 +155,11 @@ def test_tf_mode_matches_libpng_restatement_and_decodes():
              _latentish(rng, (2, 128, 256)),              # a 256^2 image's plane (> 16 KiB: window 15)
              rng.integers(0, 256, (2, 90, 200), dtype=np.uint8),  # several 8 KiB IDATs
              rng.integers(0, 256, (2, 1, 1), dtype=np.uint8),     # the smallest window
-             _latentish(rng, (2, 9, 13, 3))]
+             _latentish(rng, (2, 9, 13, 3)),
+             rng.integers(0, 256, (3, 1, 300), dtype=np.uint8),   # one row: None / Sub only
+             rng.integers(0, 256, (3, 200, 1), dtype=np.uint8),   # one column: None / Up only
+             rng.integers(0, 256, (2, 1, 50, 3), dtype=np.uint8),
+             rng.integers(0, 256, (2, 60, 1, 3), dtype=np.uint8)]
     for a in cases:
         got = png_encode(a, threads=2, mode="tf")
         sizes = png_sizes(a, threads=2, mode="tf")
