@@ -577,16 +577,10 @@ def main():
                 "share_of_step": round(kern[dom][0] / (el / args.steps * 1e3), 4),
                 "peak_basis": ("dense f16 MFMA 2.5 PFLOP/s / 3 passes (algorithmic fp32 FLOP)"
                                if args.precision == "f16x3" else "dense fp32 MFMA 157.3 TFLOP/s")}
-    # the fused k3 pair on Winograd F(2,3) along y (NIC_K3P=w, planes up to 64 columns; the
-    # default is the direct 9-tap pair) issues 2/3 of the direct form's split-f16 MFMAs: frac
-    # stays algorithmic FLOP / peak (the effective rate), issued_frac is what the matrix cores ran
-    k3_wino = (args.precision == "f16x3" and os.environ.get("NIC_K3P", "")[:1] == "w"
-               and os.environ.get("NIC_WS", "1")[:1] != "0" and W // 4 <= 64)
-    if dom == "k3_pair":
-        roofline["k3_form"] = "winograd F(2,3) along y" if k3_wino else "direct 9-tap"
-        issued = dom_flop * (2.0 / 3.0 if k3_wino else 1.0)
-        roofline["issued_tflops"] = round(issued / (dom_ms * 1e-3) / 1e12, 2)
-        roofline["issued_frac"] = round(issued / (dom_ms * 1e-3) / 1e12 / peak, 4)
+    if dom == "k3_pair":  # the direct 9-tap pair issues exactly the algorithmic products
+        roofline["k3_form"] = "direct 9-tap"
+        roofline["issued_tflops"] = round(dom_flop / (dom_ms * 1e-3) / 1e12, 2)
+        roofline["issued_frac"] = round(dom_flop / (dom_ms * 1e-3) / 1e12 / peak, 4)
     others = sorted((k for k in kern if k != dom), key=lambda k: -kern[k][0])
     if others:  # the next kernel by device time, for continuity with earlier lines (dconv7)
         k2 = others[0]

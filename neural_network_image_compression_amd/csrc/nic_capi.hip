@@ -240,32 +240,6 @@ int repack_kernel(const LayerSpec& L, const float* K, std::vector<float>& out, s
   return repack_x3(outx, 25, cin, cout, get);
 }
 
-// Winograd F(2,3)-along-y kernels of a k3 s1 layer (the fused pair's default form,
-// nic_kernels.hip conv_k3wino_kernel): taps t = 3 xi + kx of
-//   U0 = g0, U1 = ((g0 + g1) + g2) / 2, U2 = ((g0 - g1) + g2) / 2, U3 = g2   (g_ky = kernel row ky)
-// in fp32 from the layer's conv-form kernel (Conv2DTranspose k3 s1: flipped taps, swapped
-// channels, as repack_kernel), then split like any split-f16 kernel.  Returns k of 2^k.
-int repack_wino(const LayerSpec& L, const float* K, std::vector<uint16_t>& outx) {
-  const int k = 3, cin = L.cin, cout = L.cout;
-  auto conv = [&](int t, int ci, int co) {
-    if (!L.transposed) return K[((size_t)t * cin + ci) * cout + co];
-    const int ky = k - 1 - t / k, kx = k - 1 - t % k;
-    return K[(((size_t)ky * k + kx) * cout + co) * cin + ci];
-  };
-  auto get = [&](int t, int ci, int co) {
-    const int xi = t / 3, kx = t % 3;
-    const float g0 = conv(kx, ci, co), g1 = conv(3 + kx, ci, co), g2 = conv(6 + kx, ci, co);
-    switch (xi) {
-      case 0: return g0;
-      case 1: return ((g0 + g1) + g2) * 0.5f;
-      case 2: return ((g0 - g1) + g2) * 0.5f;
-      default: return g2;
-    }
-  };
-  return repack_x3(outx, 12, cin, cout, get);
-}
-bool has_wino(int id) { return id == L_CONV3 || id == L_CONV4 || id == L_DCONV5 || id == L_DCONV6; }
-
 struct SamePad {
   int out, lo;
 };
@@ -297,8 +271,6 @@ struct nic_ctx {
   float* wb[L_COUNT] = {};  // [2 models][cout]
   uint16_t* wx[L_COUNT] = {};  // split-f16 kernels [2 models][taps*cin*cout*2]
   float wscale[L_COUNT][2] = {};  // 2^-k per model for the split-f16 kernels
-  uint16_t* wxw[L_COUNT] = {};    // k3 s1 layers: Winograd U kernels [2 models][12*cin*cout*2] (repack_wino)
-  float wscalew[L_COUNT][2] = {};
   // dconv8 as the B operand of dconv7's fused projection: [2 models][2 tap blocks][2 k32][hi,lo][64][8]
   uint16_t* wproj = nullptr;
   int precision = NIC_PRECISION_F16X3;
@@ -328,19 +300,8 @@ struct nic_ctx {
   // call, read back and accumulated by nic_layer_times
   // host-array surface (nic_encode_host / nic_decode_host): its own copy-in, compute and
   // copy-out streams, per-chunk events, pinned staging and device buffers, grown on demand
-  hipStream_t hs[4] = {};  // H2D, compute (even chunks), D2H, compute (odd chunks)
+  hipStream_t hs[3] = {};  // H2D, compute, D2H
   hipEvent_t hev[3][kHostMaxChunks] = {};
-  // the odd chunks' pass state (activation regions, range-guard words and epoch): swapped into
-  // ws / ws_bytes / range / epoch around their launches, so two chunk passes can run at once on
-  // the two compute streams (host_pipeline)
-  struct PassSlot {
-    char* ws = nullptr;
-    size_t ws_bytes = 0;
-    int* range = nullptr;
-    int epoch = 0;
-  } alt;
-  int* alt_host = nullptr;  // pinned read-back of alt.range
-  hipEvent_t hev_alt = nullptr;  // alt.range's read-back done
   hipEvent_t hev_caller = nullptr;
   uint8_t* pin_in = nullptr;
   uint8_t* pin_out = nullptr;
@@ -547,15 +508,6 @@ int nic_create(int device, nic_ctx** out) {
       (void)hipMemset(c->wb[L.id], 0, bb);
       (void)hipMemset(c->wx[L.id], 0, xb);
       c->wscale[L.id][0] = c->wscale[L.id][1] = 1.0f;
-      if (has_wino(L.id)) {
-        const size_t wb = 2 * 12 * (size_t)L.cin * L.cout * 2 * sizeof(uint16_t);
-        if (hipMalloc(&c->wxw[L.id], wb) != hipSuccess) {
-          nic_destroy(c);
-          return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
-        }
-        (void)hipMemset(c->wxw[L.id], 0, wb);
-        c->wscalew[L.id][0] = c->wscalew[L.id][1] = 1.0f;
-      }
     }
   }
   if (hipMalloc(&c->wproj, 2 * kProjFrag * 2) != hipSuccess || hipMemset(c->wproj, 0, 2 * kProjFrag * 2) != hipSuccess) {
@@ -595,7 +547,6 @@ int nic_destroy(nic_ctx* c) {
     if (c->wk[i]) (void)hipFree(c->wk[i]);
     if (c->wb[i]) (void)hipFree(c->wb[i]);
     if (c->wx[i]) (void)hipFree(c->wx[i]);
-    if (c->wxw[i]) (void)hipFree(c->wxw[i]);
   }
   if (c->ws) (void)hipFree(c->ws);
   if (c->counts) (void)hipFree(c->counts);
@@ -605,19 +556,15 @@ int nic_destroy(nic_ctx* c) {
   if (c->wproj) (void)hipFree(c->wproj);
   if (c->range) (void)hipFree(c->range);
   if (c->range_host) (void)hipHostFree(c->range_host);
-  if (c->alt.ws) (void)hipFree(c->alt.ws);
-  if (c->alt.range) (void)hipFree(c->alt.range);
-  if (c->alt_host) (void)hipHostFree(c->alt_host);
   for (int i = 0; i < L_COUNT; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
   for (int i = 0; i < 3; ++i)
     for (int k = 0; k < kHostMaxChunks; ++k)
       if (c->hev[i][k]) (void)hipEventDestroy(c->hev[i][k]);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 3; ++i)
     if (c->hs[i]) (void)hipStreamDestroy(c->hs[i]);
   if (c->hev_caller) (void)hipEventDestroy(c->hev_caller);
-  if (c->hev_alt) (void)hipEventDestroy(c->hev_alt);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->hdev) (void)hipFree(c->hdev);
@@ -651,13 +598,6 @@ int nic_set_weights(nic_ctx* c, int model_id, const char* layer, const float* ho
       HIP_TRY(hipMemcpy(c->wx[L->id] + m * packedx.size(), packedx.data(), packedx.size() * sizeof(uint16_t),
                         hipMemcpyHostToDevice));
       c->wscale[L->id][m] = std::ldexp(1.0f, -kexp);
-    }
-    if (has_wino(L->id)) {
-      std::vector<uint16_t> wino;
-      const int kw = repack_wino(*L, host, wino);
-      HIP_TRY(hipMemcpy(c->wxw[L->id] + m * wino.size(), wino.data(), wino.size() * sizeof(uint16_t),
-                        hipMemcpyHostToDevice));
-      c->wscalew[L->id][m] = std::ldexp(1.0f, -kw);
     }
     if (L->id == L_DCONV8) {
       const std::vector<uint16_t> f = proj_fragments(packed, kexp);
@@ -724,33 +664,12 @@ bool use_k3pair() {
   }();
   return on;
 }
-// NIC_K3P=w: the fused pair on Winograd F(2,3) along y where it applies (planes up to 64
-// columns).  Not the default: measured slower than the direct pair (0.304 vs 0.261 ms per
-// launch, same box) -- both layers' U kernels (384 VGPRs per 16 channels)
-// leave one wave per SIMD, so its transform / epilogue VALU (PMC: 4.0 per MFMA) cannot overlap
-// a partner's MFMAs (MFMA busy 0.34 vs 0.71).
-bool use_k3wino() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_K3P");
-    return use_k3pair() && e && e[0] == 'w';
-  }();
-  return on;
-}
-// the fused k3 residual pair of one encoder / decoder pass: Winograd when it takes the plane
-hipError_t launch_pair(nic_ctx* c, ConvArgs ap, LayerId la, LayerId lb, int h, int w, hipStream_t st) {
+// the fused k3 residual pair of one encoder / decoder pass
+hipError_t launch_pair(nic_ctx* c, ConvArgs ap, LayerId lb, hipStream_t st) {
   ap.wx2 = c->wx[lb];
   ap.wscale2[0] = c->wscale[lb][0];
   ap.wscale2[1] = c->wscale[lb][1];
   ap.bias2 = c->wb[lb];
-  if (use_k3wino() && k3wino_supported(h, w)) {
-    ap.wxw = c->wxw[la];
-    ap.wscalew[0] = c->wscalew[la][0];
-    ap.wscalew[1] = c->wscalew[la][1];
-    ap.wxw2 = c->wxw[lb];
-    ap.wscalew2[0] = c->wscalew[lb][0];
-    ap.wscalew2[1] = c->wscalew[lb][1];
-    return launch_k3wino_x3(ap, st);
-  }
   return launch_k3pair_x3(ap, st);
 }
 
@@ -857,7 +776,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {
     // conv3 -> conv4 -> + res as one launch (R1 -> R3, the residual read from the input
     // rows in LDS); timed as conv4
-    TIMED(L_CONV4, launch_pair(c, conv(L_CONV3, R[1], R[3], nullptr, h2, w2, h2, w2, 1, 1), L_CONV3, L_CONV4, h2, w2, st));
+    TIMED(L_CONV4, launch_pair(c, conv(L_CONV3, R[1], R[3], nullptr, h2, w2, h2, w2, 1, 1), L_CONV4, st));
   } else {
     TIMED(L_CONV3, run(L_CONV3, conv(L_CONV3, R[1], R[2], nullptr, h2, w2, h2, w2, 1, 1)));
     TIMED(L_CONV4, run(L_CONV4, conv(L_CONV4, R[2], R[3], R[1], h2, w2, h2, w2, 1, 1)));
@@ -929,7 +848,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   TIMED(L_DCONV1, run(L_DCONV1, d1));
   const int h2 = 2 * h8, w2 = 2 * w8;
   if (x3 && use_k3pair() && k3pair_supported(h2, w2)) {  // dconv5 -> dconv6 -> + res, timed as dconv6
-    TIMED(L_DCONV6, launch_pair(c, conv(L_DCONV5, R[1], R[3], nullptr, h2, w2, h2, w2), L_DCONV5, L_DCONV6, h2, w2, st));
+    TIMED(L_DCONV6, launch_pair(c, conv(L_DCONV5, R[1], R[3], nullptr, h2, w2, h2, w2), L_DCONV6, st));
   } else {
     TIMED(L_DCONV5, run(L_DCONV5, conv(L_DCONV5, R[1], R[2], nullptr, h2, w2, h2, w2)));
     TIMED(L_DCONV6, run(L_DCONV6, conv(L_DCONV6, R[2], R[3], R[1], h2, w2, h2, w2)));
@@ -982,14 +901,6 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
 // resp. 2h8 x 2w8) must stay under 2^30 bytes, i.e. about 67 MP per image.  Larger images
 // run the exact-fp32 kernels (64-bit addressing) instead of failing (nic.h).
 bool x3_plane_fits(long long h64, long long w64) { return h64 * w64 * 64 * 4 < (1LL << 30); }
-
-// Swap the host pipeline's second pass slot into (or back out of) the ctx fields the passes use.
-void swap_slot(nic_ctx* c) {
-  std::swap(c->ws, c->alt.ws);
-  std::swap(c->ws_bytes, c->alt.ws_bytes);
-  std::swap(c->range, c->alt.range);
-  std::swap(c->epoch, c->alt.epoch);
-}
 
 // The chained re-run's barrier timeout (nic_kernels.hip grid_barrier), read from words[4] of
 // c->range with the device idle: reported once as NIC_EHIP, and the barrier words (arrivals,
@@ -1156,17 +1067,9 @@ class CopyPool {
   std::condition_variable cv_;
 };
 
-// NIC_HOST_SLOTS=2 (A/B): odd chunks on a second compute stream with the second pass slot.
-// Not the default: measured slower (round trip 2.15-2.20 vs 1.93-1.96 ms, decode 1.21 vs 1.06
-// ms, profiles/r4_ab_logs.txt) -- two chunk passes' persistent kernels (one block per CU each)
-// contend for the CUs instead of filling each other's tails.
-bool host_two_slots() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_HOST_SLOTS");
-    return e && e[0] == '2';
-  }();
-  return on;
-}
+// (A second pass slot on a second compute stream, so chunk k+1's kernels could fill chunk k's
+// tails, measured slower in round 4 -- round trip 2.15-2.20 vs 1.93-1.96 ms: two chunk passes'
+// persistent kernels, one block per CU each, contend for the CUs -- and was removed.)
 
 // Host-side wait for an event: polling hipEventQuery (default) returns as soon as the GPU
 // signals, where hipEventSynchronize may sleep and pay a wake-up latency per chunk
@@ -1185,20 +1088,12 @@ hipError_t host_wait(hipEvent_t e) {
 }
 
 int host_setup(nic_ctx* c) {
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 3; ++i)
     if (!c->hs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking));
   for (int i = 0; i < 3; ++i)
     for (int k = 0; k < kHostMaxChunks; ++k)
       if (!c->hev[i][k]) HIP_TRY(hipEventCreateWithFlags(&c->hev[i][k], hipEventDisableTiming));
   if (!c->hev_caller) HIP_TRY(hipEventCreateWithFlags(&c->hev_caller, hipEventDisableTiming));
-  if (!c->hev_alt) HIP_TRY(hipEventCreateWithFlags(&c->hev_alt, hipEventDisableTiming));
-  if (!c->alt.range) {
-    if (hipMalloc(&c->alt.range, 8 * sizeof(int)) != hipSuccess || hipMemset(c->alt.range, 0, 8 * sizeof(int)) != hipSuccess ||
-        hipHostMalloc(&c->alt_host, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      return fail(NIC_ENOMEM, "host surface: second pass slot allocation failed");
-    }
-  }
   return NIC_OK;
 }
 
@@ -1230,13 +1125,9 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   std::vector<int> lo;
   host_chunk_plan(n, chunks, lo);
   const int K = (int)lo.size() - 1;
-  // NIC_HOST_SLOTS=2: odd chunks on the second compute stream with the second pass slot
-  const bool two = host_two_slots() && K > 1;
-  hipStream_t cs[2] = {c->hs[1], two ? c->hs[3] : c->hs[1]};
   HIP_TRY(hipEventRecord(c->hev_caller, caller));
   HIP_TRY(hipStreamWaitEvent(c->hs[0], c->hev_caller, 0));
   HIP_TRY(hipStreamWaitEvent(c->hs[1], c->hev_caller, 0));
-  if (two) HIP_TRY(hipStreamWaitEvent(c->hs[3], c->hev_caller, 0));
   int err = NIC_OK, issued = 0;
   for (int k = 0; k < K && !err; ++k) {
     const size_t i0 = lo[k] * in_row, ib = (lo[k + 1] - lo[k]) * in_row;
@@ -1246,19 +1137,16 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
       CopyPool::get().copy(c->pin_in + i0, in + i0, ib);
       src = c->pin_in + i0;
     }
-    const int sl = two ? (k & 1) : 0;
     hipError_t e = hipMemcpyAsync(d_in + i0, src, ib, hipMemcpyHostToDevice, c->hs[0]);
     if (e == hipSuccess) e = hipEventRecord(c->hev[0][k], c->hs[0]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(cs[sl], c->hev[0][k], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[1], c->hev[0][k], 0);
     if (e != hipSuccess) {
       err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
       break;
     }
-    if (sl) swap_slot(c);
-    err = pass(d_in + i0, lo[k + 1] - lo[k], d_out + o0, cs[sl]);
-    if (sl) swap_slot(c);
+    err = pass(d_in + i0, lo[k + 1] - lo[k], d_out + o0, c->hs[1]);
     if (err) break;
-    e = hipEventRecord(c->hev[1][k], cs[sl]);
+    e = hipEventRecord(c->hev[1][k], c->hs[1]);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->hs[2], c->hev[1][k], 0);
     if (e == hipSuccess)
       e = hipMemcpyAsync(out_pin ? out + o0 : c->pin_out + o0, d_out + o0, ob, hipMemcpyDeviceToHost, c->hs[2]);
@@ -1274,9 +1162,7 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   const bool chain_check = !err && issued > 0 && c->precision == NIC_PRECISION_F16X3 &&
                            c->range_policy == NIC_RANGE_FALLBACK;
   if (chain_check && (hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess ||
-                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess ||
-                      (two && (hipMemcpyAsync(c->alt_host, c->alt.range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[3]) != hipSuccess ||
-                               hipEventRecord(c->hev_alt, c->hs[3]) != hipSuccess))))
+                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess))
     err = fail(NIC_EHIP, "host surface: range-word read-back failed");
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
     hipError_t e = host_wait(c->hev[2][k]);
@@ -1291,20 +1177,13 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
   // (~10-30 us per call); any error path drains them
   if (!err && issued == K && chain_check) {
     hipError_t e = host_wait(c->hev_caller);
-    if (e == hipSuccess && two) e = host_wait(c->hev_alt);
     if (e != hipSuccess) err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
   }
   if (err || issued != K)
-    for (int i = 0; i < 4; ++i) (void)hipStreamSynchronize(c->hs[i]);
-  if (!err && chain_check && (c->range_host[4] || (two && c->alt_host[4]))) {
+    for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);
+  if (!err && chain_check && c->range_host[4]) {
     HIP_TRY(hipDeviceSynchronize());
     err = chain_timeout_check(c, c->range_host, "host surface");
-    if (two && c->alt_host[4]) {
-      swap_slot(c);
-      const int e2 = chain_timeout_check(c, c->alt_host, "host surface");
-      swap_slot(c);
-      if (!err) err = e2;
-    }
   }
   return err;
 }
@@ -1636,18 +1515,10 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   if (!c || !passes) return fail(NIC_EINVAL, "nic_range_trips: NULL argument");
   DeviceGuard guard(c->device);
   HIP_TRY(hipDeviceSynchronize());
-  int words[5] = {}, alt[5] = {};
+  int words[5] = {};
   HIP_TRY(hipMemcpy(words, c->range, sizeof(words), hipMemcpyDeviceToHost));
-  if (c->alt.range) HIP_TRY(hipMemcpy(alt, c->alt.range, sizeof(alt), hipMemcpyDeviceToHost));
-  *passes = (int64_t)words[1] + alt[1] + c->error_trips;
-  int rc = chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
-  if (alt[4]) {  // the host pipeline's second slot
-    swap_slot(c);
-    const int rc2 = chain_timeout_check(c, alt, "nic_range_trips");
-    swap_slot(c);
-    if (!rc) rc = rc2;
-  }
-  return rc;
+  *passes = (int64_t)words[1] + c->error_trips;
+  return chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
 }
 
 int nic_rerun_launch_info(nic_ctx* c, int* blocks_per_cu, int* grid, int* cooperative) {

@@ -63,19 +63,12 @@ struct ConvArgs {
   // the counts [3 nimg][256], zero on entry, added to with device-scope atomics
   uint32_t* hist_part;
   int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
-  int d1_mixed;           // dconv1_all: one block group over both models' tiles (weights reloaded at the switch)
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
   const uint16_t* wx2;
   float wscale2[2];
   const float* bias2;
   int seg_rows;
-  // the pair on Winograd F(2,3) along y: both layers' U kernels [2 models][12 taps (xi, kx)]
-  // [Cin/16][hi,lo][2][Cout][8] of U*2^k and their 2^-k (nic_capi.hip repack_wino)
-  const uint16_t* wxw;
-  float wscalew[2];
-  const uint16_t* wxw2;
-  float wscalew2[2];
   // conv1 fused into conv2 (f16x3): the colour plane is computed from the RGB input and
   // conv1's split output is written straight into conv2's LDS halo (no HBM round trip)
   const uint8_t* rgb;     // [N][H0][W0][3]
@@ -150,9 +143,6 @@ hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st);   // 
 // one launch (split-f16), for planes up to K3P_MAX_W columns; false: use two launches
 bool k3pair_supported(int H, int W);
 hipError_t launch_k3pair_x3(const ConvArgs& a, hipStream_t st);
-// the same pair on Winograd F(2,3) along y (planes up to 64 columns; a.wxw / a.wxw2 set)
-bool k3wino_supported(int H, int W);
-hipError_t launch_k3wino_x3(const ConvArgs& a, hipStream_t st);
 hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st);  // conv1 fused into conv2 (f16x3)
 // the fused conv1's padded colour planes: origin offsets and plane size in f16 elements
 // (a.cplane must hold 2 * P * hp * wp of them)

@@ -2163,15 +2163,6 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 constexpr int C12_PPW = 21;                          // patch row pitch in dwords (42 f16 columns)
 constexpr int C12_PPIECE = (C12_PH * C12_PPW + 63) / 64;  // 1-dword-per-lane DMA pieces per plane (14)
 constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in LDS (hi or lo)
-#ifndef NIC_C12_E3
-// 1 (A/B build): pixel tile MT-1's conv2 epilogue runs on the ts 1 wave (at the top of the next
-// tile, from its own sums kept in registers and the ts 0 wave's sums of that tile left in LDS)
-// instead of on the ts 0 wave, whose chain is the longer one by stamps (7,843 vs 6,734 cycles
-// per tile, profiles/r3n_c12_stamps.txt).  Measured slower: conv12 0.236-0.238 vs 0.228-0.230
-// ms (3 alternating rounds), 4K 3.89 vs 3.62 ms (profiles/r4_ab_logs.txt) -- the ts 1 wave's
-// patch DMA and stream start later, and that delay reaches the next barrier.
-#define NIC_C12_E3 0
-#endif
 #ifndef NIC_C12_PT0
 #define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
 #endif
@@ -2179,16 +2170,6 @@ constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in
 // ts 0's conv2 stream at priority 2 over ts 1's: conv12 0.2433-0.2441 vs 0.2446-0.2459 ms (3
 // alternating rounds, profiles/r4_ab_logs.txt); 0 (A/B build): both at priority 1
 #define NIC_C12_PRIO 1
-#endif
-#ifndef NIC_C12_U0
-// A/B build (> 0): conv1 shares in half-tile units (pixel tile x 16-channel tile: 46 per tile)
-// instead of whole pixel tiles, NIC_C12_U0 units per ts 0 wave, the ts 1 waves the rest -- to
-// even out the ts 0 chain (7,843 cycles per tile) and the ts 1 chain (6,664,
-// profiles/r4n_c12_stamps.txt).  Measured slower: conv12 0.264-0.269 vs 0.237-0.243 ms, 4K 4.17 vs
-// 3.74 ms (profiles/r4_ab_logs.txt): every unit re-reads its pixel tile's im2col fragments
-// (8 ds_read_b32, 2-way conflicted) and runs one 3-MFMA chain instead of two, so a unit costs far
-// more than half a tile.  0: whole pixel tiles (NIC_C12_PT0).
-#define NIC_C12_U0 0
 #endif
 
 // Padded colour planes of the fused conv1 (ConvArgs::cplane): origin offsets and sizes in
@@ -2244,9 +2225,6 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   char* part = lds + 2 * G::HALO_BYTES;           // [NCG] partial tiles of the ts = 1 waves
   char* patches = part + NCG * PART;              // [2 parities][hi, lo] patch planes
   int* pflag = (int*)(patches + 4 * C12_PLANE);   // [NCG] last tile whose partials ts 0 has read
-  // NIC_C12_E3: the ts 0 waves' sums of pixel tile MT-1 for the ts 1 wave [2 parities][NCG][1 KB]
-  char* part3 = (char*)(pflag + 4);
-  constexpr int E_MT = NIC_C12_E3 ? MT - 1 : MT;  // pixel tiles whose epilogue ts 0 runs
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -2302,10 +2280,6 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     }
   }
   const float scale1 = a.wscale1[model];
-  // NIC_C12_U0: a wave's units (base + cg + 4k) all have channel tile (base + cg) & 1
-  const int uct = (TS == 0 ? cg : 20 + cg) & 1;
-  const f16x8 A1u_hi = uct ? A1[1][0] : A1[0][0], A1u_lo = uct ? A1[1][1] : A1[0][1];
-  const f32x4 b1u = uct ? b1[1] : b1[0];
   int poff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -2349,59 +2323,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     constexpr int NPT = (G::HH * G::HW + 15) / 16, PT0 = NIC_C12_PT0, PT1 = (NPT - 4 * PT0 + 3) / 4;
     static_assert(PT0 >= 0 && PT1 >= 0 && 4 * (PT0 + PT1) >= NPT, "conv1 shares cover the halo");
     constexpr int PTW = TS == 0 ? PT0 : PT1, PTB = TS == 0 ? 0 : 4 * PT0;
-    // half-tile units: unit v = (pixel tile v >> 1, channel tile v & 1); this wave's units
-    // UB + cg + 4k, k < UW (all of channel tile uct)
-    constexpr int NU = 2 * NPT, U0 = NIC_C12_U0, U1 = (NU - 4 * U0 + 3) / 4;
-    constexpr int UW = TS == 0 ? U0 : U1, UB = TS == 0 ? 0 : 4 * U0;
-    static_assert(U0 >= 0 && U1 >= 0 && 4 * (U0 + U1) >= NU, "conv1 unit shares cover the halo");
-    if constexpr (NIC_C12_U0 > 0 && UW > 0) {
-      int p, t0y, t0x;
-      tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
-      char* halo = lds + (i & 1) * G::HALO_BYTES;
-      const char* ph = patches + (i & 1) * 2 * C12_PLANE;
-      const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;
-      f16x8 bh[UW], bl[UW];
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        const int q = 16 * ((UB + cg + 4 * u) >> 1) + l16;
-        const int qq = q < G::HH * G::HW ? q : 0;
-        const int hy = qq / G::HW, hx = qq - hy * G::HW;
-        const char* pb = ph + (2 * hy * C12_PPW + hx) * 4;
-        u32x4 H, L;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          H[j] = *(const uint32_t*)(pb + poff[j]);
-          L[j] = *(const uint32_t*)(pb + C12_PLANE + poff[j]);
-        }
-        bh[u] = __builtin_bit_cast(f16x8, H);
-        bl[u] = __builtin_bit_cast(f16x8, L);
-      }
-      f32x4 c1[UW];
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {  // the same MFMA chain as the whole-tile form, per channel tile
-        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_lo, bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_hi, bl[u], c1[u], 0, 0, 0);
-        c1[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1u_hi, bh[u], c1[u], 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        const int v = UB + cg + 4 * u;
-        if (v >= NU) break;  // wave-uniform
-        const int q = 16 * (v >> 1) + l16;
-        const bool qv = q < G::HH * G::HW;
-        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
-        const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
-        f32x4 vv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) vv[r] = in1 ? leaky02(scale_bias(c1[u][r], scale1, b1u[r])) : 0.f;
-        range_track(rmax, vv);
-        f16x4 hi, lo;
-        split4(vv, hi, lo);
-        const u32x4 q16 = swap16_pair(hi, lo);
-        if (qv)
-          *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * uct + 4 * (g & ~1)) * 2) = q16;
-      }
-    } else if constexpr (NIC_C12_U0 == 0 && PTW > 0) {
+    if constexpr (PTW > 0) {
       int p, t0y, t0x;
       tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
       char* halo = lds + (i & 1) * G::HALO_BYTES;
@@ -2496,19 +2418,17 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
     __builtin_amdgcn_s_setprio(0);
   };
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
-  // epilogue of tile i (called for i = 0, 1, 2, ... in order by each role): ts 0 runs pixel
-  // tiles [0, E_MT) from its own sums + the ts 1 partials; with NIC_C12_E3 the ts 1 wave runs
-  // pixel tile MT-1 from its own sums + the ts 0 sums in part3 (a + b == b + a: same bits)
+  // epilogue of tile i (called for i = 0, 1, 2, ... in order by the ts 0 waves): its own sums +
+  // the ts 1 partials
   auto epilogue = [&](int i) {
     int p, t0y, t0x;
     tile_take(w_ep, p, t0y, t0x);
-    constexpr int M0 = TS == 0 ? 0 : E_MT, M1 = TS == 0 ? E_MT : MT;
-    const char* pp = TS == 0 ? part + cg * PART + lane * 16 : part3 + ((i & 1) * NCG + cg) * 1024 + lane * 16 - M0 * 1024;
+    const char* pp = part + cg * PART + lane * 16;
     f32x4 q4[MT];  // all partial reads in flight before the first use
 #pragma unroll
-    for (int m = M0; m < M1; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
+    for (int m = 0; m < MT; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
 #pragma unroll
-    for (int m = M0; m < M1; ++m) {
+    for (int m = 0; m < MT; ++m) {
       const f32x4 q = q4[m];
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
@@ -2573,12 +2493,8 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
       stream(i);
-      if constexpr (NIC_C12_E3)  // this wave's sums of pixel tile MT-1 for the ts 1 wave
-        *(f32x4*)(part3 + ((i & 1) * NCG + cg) * 1024 + lane * 16) = acc[MT - 1];
       C12_MARK(5);
     } else {
-      if constexpr (NIC_C12_E3)
-        if (i > 0) epilogue(i - 1);  // pixel tile MT-1 of tile i-1 (its sums still in acc)
       if (i == ntile) break;
       if (i + 2 < ntile) patch_dma(i + 2);  // into the buffer conv1(i) read; lands during the stream
       C12_MARK(4);
@@ -2590,7 +2506,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       C12_MARK(2);
       char* pp = part + cg * PART + lane * 16;
 #pragma unroll
-      for (int m = 0; m < E_MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
       if (i + 1 < ntile) conv1(i + 1);
       C12_MARK(3);
       dma_wait_all();  // patch i+2 landed (before B_top(i+1) publishes it)
@@ -2624,7 +2540,7 @@ __device__ __forceinline__ int xcd_pos(int b, int nb) {
 __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
   using G = GeomS2<32, 8, 8>;
   __shared__ __attribute__((aligned(16)))
-  char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16 + (NIC_C12_E3 ? 2 * 4 * 1024 : 0)];
+  char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -2894,10 +2810,10 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cg = wave & 3;
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   const int per_plane = a.tiles_y * a.tiles_x;
-  // d1_mixed: one group walks both models' planes (Y first), the weights reloaded when a tile
-  // of the other model comes up -- 12 tiles for every block at config 2 instead of 13 for a few
-  // Y blocks (1,024 Y tiles cannot split evenly over 85 of 256 blocks)
-  const int p0 = a.d1_mixed ? 0 : model ? a.nimg : 0, np = a.d1_mixed ? a.P : model ? a.P - a.nimg : a.nimg;
+  // (one group walking both models' planes with the weights reloaded at the switch -- 12 tiles
+  // for every block at config 2 instead of 13 for a few Y blocks -- measured slower, round 4:
+  // dconv1 0.0604-0.0608 vs 0.0555-0.0567 ms, the mid-walk reload costs more than the tail)
+  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
   const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
   if (ntile == 0) return;  // block-uniform
@@ -2905,7 +2821,6 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
   f16x8 w1[NT1][2], w2[NT2][2];
   float scale;
   f32x4 bias;
-  int cur = -1;  // model of the resident weights
   auto load_weights = [&](int m) __attribute__((always_inline)) {
     const char* wsrc = (const char*)a.wx + (size_t)m * 25 * TAP_BYTES;
     auto frag_w = [&](int tap, int hl) {
@@ -2921,9 +2836,8 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
       for (int hl = 0; hl < 2; ++hl) w2[t][hl] = frag_w(TB2 + t, hl);
     scale = a.wscale[m] * 0.0039215688593685627f;  // 2^-k and the dequantiser's 1/255
     bias = *(const f32x4*)(a.bias + m * COUT + cg * 16 + 4 * g);
-    cur = m;
   };
-  if (!a.d1_mixed) load_weights(model);
+  load_weights(model);
 
   // code staging: thread q = threadIdx.x + 512 j loads dword q & 7 of halo pixel q >> 3
   int st_lds[D1A_LD], st_hy[D1A_LD], st_hx[D1A_LD];
@@ -3021,10 +2935,6 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     stage_barrier();  // tile i's halo complete; tile i-2's reads of this buffer done everywhere
     int pl, ty, tx;
     it_run.take(pl, ty, tx);
-    if (a.d1_mixed) {  // wave-uniform: the tile's model
-      const int m = p0 + pl >= a.nimg ? 1 : 0;
-      if (m != cur) load_weights(m);
-    }
     if constexpr (NIC_D1A_PF == 2) {
       if (i + 2 < ntile) load_codes(cq);  // tile i+2: lands during this tile's and the next's MFMAs
     } else {  // A/B build: one tile ahead
@@ -3100,12 +3010,6 @@ __device__ __forceinline__ int k3p_off(int rec, int chunk) { return rec * K3P_RE
 // columns (a.tiles_x of them); per strip the input rows carry 66 columns (2 each side), conv_a
 // computes 64 (the strip's 62 plus the column either side conv_b needs, zeros outside the
 // plane) and conv_b the strip's 62 (3 % of its lanes and 3 % of conv_a's work are the seams).
-#ifndef NIC_K3P_PRIO
-// 1 (A/B build): conv_b's MFMA stream at priority 2 over conv_a's.  Measured slower: conv4 /
-// dconv6 0.261-0.264 vs 0.258-0.260 ms (3 alternating rounds, profiles/r4_ab_logs.txt) -- conv_a's
-// stream then finishes later, and so does its epilogue writing the rows conv_b needs next step.
-#define NIC_K3P_PRIO 0
-#endif
 // Row ranges of the pair's blocks balanced by pipeline steps (launch_k3pair_x3): block b takes
 // rows [start[b], start[b + 1]) of the stream; start[0] < 0: the plain equal-rows split
 constexpr int K3P_MAX_GRID = 320;
@@ -3231,12 +3135,9 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a, K3Range
       fb[m][0] = frag(m, 0, 0);
       fb[m][1] = frag(m, 0, 1);
     });
-    // NIC_K3P_PRIO: conv_b's stream (the role on the step's critical path by stamps: conv_a waits
-    // ~2,660 cycles per step at the barrier) outranks conv_a's when both have an MFMA ready
-    if (NIC_K3P_PRIO && role == 1)
-      __builtin_amdgcn_s_setprio(2);
-    else
-      __builtin_amdgcn_s_setprio(1);
+    // (conv_b's stream at priority 2 over conv_a's measured 1 % slower: conv_a's stream, and with
+    // it the epilogue writing the rows conv_b needs next step, then finishes later; round 4)
+    __builtin_amdgcn_s_setprio(1);
     static_for<NSTEP>([&](auto stc) {
       constexpr int st = decltype(stc)::value, t = st / KST, ks = st % KST;
       static_for<MT>([&](auto mc) {
@@ -3443,495 +3344,10 @@ bool k3pair_supported(int H, int W) {
   return H > 0 && W > 0 && k3pair_strips(W) > 0 && (long long)H * W * K3P_REC < (1LL << 31);
 }
 
-// ------------------------------------------------------------------------------------
-// Fused k3 residual pair on Winograd F(2,3) along y (round 4; NIC_K3P=w, planes up to 64
-// columns; measured slower than the direct pair above, which stays the default: 0.304 vs
-// 0.261 ms, one wave per SIMD leaves the transform VALU unhidden -- DESIGN section 5b).  conv3 -> conv4 -> + x and
-// dconv5 -> dconv6 -> + x (encoder.py:22-25, decoder.py:26-29) with every conv computed two
-// output rows at a time:
-//   rows d0..d3 = in[y-1 .. y+2] of a pair (y, y+1):  V0 = d0 - d2, V1 = d1 + d2,
-//   V2 = d2 - d1, V3 = d1 - d3;  M_xi[x] = sum_kx sum_ci V_xi[x + kx - 1][ci] U_xi[kx][ci][co]
-//   with U0 = g0, U1 = ((g0 + g1) + g2) / 2, U2 = ((g0 - g1) + g2) / 2, U3 = g2 (g_ky the
-//   kernel row ky);  out[y] = (M0 + M1) + M2,  out[y + 1] = (M1 - M2) - M3.
-// 4 x 3 x 2 k32-steps x 3 split MFMAs per 16 pixels of a pair instead of 2 x 9 x 2 x 3: the
-// split-f16x3 products drop by 1.5x (the pair kernel sits at the chip's power limit, where
-// fewer multiplies, not fewer cycles, are the lever: DESIGN section 5).  The transformed
-// operands are split to f16 hi / lo like any activation (V within 2x of the activations) and
-// the U kernels are pre-scaled per model like the direct kernels (nic_capi.hip repack_wino).
-//
-// Block = 8 waves, one per CU, all 64 columns of a plane, a contiguous range of its row
-// pairs.  Waves 0-3 (A, conv_a, 16 output channels each) and 4-7 (B, conv_b) are SIMD
-// partners; each holds its layer's 12 U fragments x 2 k32-steps x hi / lo (192 VGPRs).  LDS:
-// VI = the four V rows of conv_a's current pair, VB = the four V rows of conv_b's, and one raw
-// input row of staging.  The steps alternate (one barrier each):
-//   A-step i: A runs pair P_i = (r0 + 2i - 1, r0 + 2i) of conv_a from VI and its epilogue
-//             builds conv_b's V rows of pair Q_{i-1} = (r0 + 2i - 2, r0 + 2i - 1) into VB;
-//             B DMAs input row r0 + 2i + 3 into the staging.
-//   B-step i: B runs Q_{i-1} from VB (+ residual, split stores to HBM); A rebuilds VI in
-//             place for P_{i+1} (input rows r0 + 2i .. r0 + 2i + 3).
-// One wave per SIMD issues MFMAs in each step while its partner does the other step's
-// vector work.  The two previous rows a V build needs are not kept anywhere: they are
-// recovered from the V rows being replaced -- d1 + d2 and d2 - d1 give d2 = (V1 + V2) / 2 and
-// d1 = (V1 - V2) / 2, then d3 = d1 - V3 -- exact up to the split rounding (~2^-22 of the
-// activations, not accumulated: each recovered row is formed afresh from a new V row).  The
-// first pair of a segment starts from a VB written to recover (a(r0 - 1), a(r0)) and a VI
-// built from four input rows.
-// Rows outside the plane are zeros (SAME padding); V records of columns -1 and >= 16 MT are
-// zero pads; columns W .. 16 MT - 1 carry zeros from the producers.
-// ------------------------------------------------------------------------------------
-constexpr int K3W_ROWB = K3P_ROWB;                  // one V row: records x = -1 .. 66 (17,408 B)
-constexpr int K3W_SETB = 4 * K3W_ROWB;              // four V rows (69,632 B)
-constexpr int K3W_STGB = 64 * K3P_REC;              // one raw input row (16,384 B)
-constexpr int K3W_LDS = 2 * K3W_SETB + K3W_STGB;    // 155,648 B
-// the epilogues and the VI build placed inside the next tile's MFMA stream (1) or after it (0;
-// 0.304 vs 0.327 ms per launch on the same box: with one wave per SIMD the interleave only
-// adds live registers, 41 vs 17 spills)
-#ifndef NIC_K3W_IL
-#define NIC_K3W_IL 0
-#endif
-constexpr bool kK3wIL = NIC_K3W_IL != 0;
-
-// a value the compiler must treat as redefined here: keeps loop-invariant addresses (lane
-// constants) from being hoisted out of the step loop and held in VGPRs across it
-template <class T>
-__device__ __forceinline__ T opaque(T v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-__device__ __forceinline__ f32x4 unsplit4(const f16x4& hi, const f16x4& lo) {
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 H = __builtin_bit_cast(u32x2, hi), L = __builtin_bit_cast(u32x2, lo);
-  return (f32x4){add_f16_pair<0>(H[0], L[0]), add_f16_pair<1>(H[0], L[0]), add_f16_pair<0>(H[1], L[1]),
-                 add_f16_pair<1>(H[1], L[1])};
-}
-// 8 channels: hi chunk h, lo chunk l (16 B each) -> fp32 of channels 2p, 2p + 1
-__device__ __forceinline__ void unsplit_pair(const u32x4& h, const u32x4& l, int p, float& v0, float& v1) {
-  v0 = add_f16_pair<0>(h[p], l[p]);
-  v1 = add_f16_pair<1>(h[p], l[p]);
-}
-// split of two fp32 values into the dword pair (hi, lo) of packed f16 (split4's per-pair body)
-__device__ __forceinline__ void split2(float v0, float v1, unsigned& h, unsigned& l) {
-  float d0, d1;
-  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(v0), "v"(v1));
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(h), "v"(v0));
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(h), "v"(v1));
-  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(d0), "v"(d1));
-}
-
-template <int MT>
-__global__ __launch_bounds__(256, 1) void conv_k3wino_kernel(ConvArgs a) {
-  constexpr int COUT = 64, KST = 2;
-  __shared__ __attribute__((aligned(16))) char lds[K3W_LDS];
-  char* vi = lds;
-  char* vb = lds + K3W_SETB;
-  char* stg = lds + 2 * K3W_SETB;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // output channels 16 w ..
-  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-  const int H = a.H, W = a.W;
-  const int hp = (H + 1) >> 1;  // row pairs per plane
-  const long long total = (long long)a.P * hp;
-  const long long per_block = (total + gridDim.x - 1) / gridDim.x;
-  const long long g0 = (long long)blockIdx.x * per_block, g1 = min(g0 + per_block, total);
-  const unsigned plane_bytes = (unsigned)(H * W) * K3P_REC;
-
-  // zero pads of both V sets: record 0 (x = -1) and records 16 MT + 1 .. (never written)
-  for (int q = threadIdx.x; q < 8 * (K3W_ROWB / 16); q += 256) {
-    const int row = q / (K3W_ROWB / 16), rq = q - row * (K3W_ROWB / 16), rec = rq >> 4;
-    if (rec == 0 || rec > 16 * MT) *(u32x4*)(lds + row * K3W_ROWB + rq * 16) = (u32x4){0u, 0u, 0u, 0u};
-  }
-
-  // B fragments: pixel 16 m + l16 at tap column kx -> record 16 m + l16 + kx of a V row; lane
-  // group g reads chunk 8 hl + 4 ks + g (the XOR with (2 hl + ks) << 6 selects hl, ks)
-  unsigned bx[3];  // per tap column: record l16 + kx with its own swizzle
-#pragma unroll
-  for (int kx = 0; kx < 3; ++kx) bx[kx] = (unsigned)k3p_off(l16 + kx, g);
-  const int chunk_st = (g & 1) * 8 + 2 * w + (g >> 1);  // this lane's 16-B granule after swap16_pair
-
-  f16x8 wa[12][KST][2], wb[12][KST][2];  // conv_a / conv_b U fragments of channels 16 w ..
-  int model = -1;
-  float scale_a = 0.f, scale_b = 0.f;
-  f32x4 bias_a = {}, bias_b = {};
-  float rmax = 0.f;
-  auto load_weights = [&](int m) __attribute__((always_inline)) {
-    constexpr int TAP_BYTES = 64 * COUT * 4;
-    const char* sa = (const char*)a.wxw + (size_t)m * 12 * TAP_BYTES;
-    const char* sb = (const char*)a.wxw2 + (size_t)m * 12 * TAP_BYTES;
-#pragma unroll
-    for (int t = 0; t < 12; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KST; ++ks)
-#pragma unroll
-        for (int hl = 0; hl < 2; ++hl) {
-          const size_t o = (size_t)t * TAP_BYTES + ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + w * 16 + l16) * 16;
-          wa[t][ks][hl] = *(const f16x8*)(sa + o);
-          wb[t][ks][hl] = *(const f16x8*)(sb + o);
-        }
-    scale_a = a.wscalew[m];
-    scale_b = a.wscalew2[m];
-    bias_a = *(const f32x4*)(a.bias + m * COUT + 16 * w + 4 * g);
-    bias_b = *(const f32x4*)(a.bias2 + m * COUT + 16 * w + 4 * g);
-  };
-
-  // M_xi of pixel tile M over a V set with the U fragments wr (xi-major, 24 steps of 3 MFMAs;
-  // B fragments read two steps ahead) into acc[M & 1]; hook(step) after every step places
-  // the previous tile's epilogue and the VI build in the stream (kK3wIL; the MFMA of one
-  // step and a slice of vector work then issue together -- one wave per SIMD has no partner
-  // whose VALU could fill the MFMA gaps)
-  f32x4 acc[4];
-  auto mfma_tile = [&](const char* set, const f16x8 (&wr)[12][KST][2], auto mc, auto&& hook) __attribute__((always_inline)) {
-    constexpr int M = decltype(mc)::value;
-    f32x4(&ac)[4] = acc;
-    __builtin_amdgcn_sched_barrier(0);  // the previous tile's epilogue stays ahead of these reads
-    hook(std::integral_constant<int, -1>{});  // before the accumulators restart: the previous tile's sums
-    const unsigned sb = lds_off(set);
-    const unsigned b0[3] = {opaque(sb + bx[0]), opaque(sb + bx[1]), opaque(sb + bx[2])};
-    auto frag = [&](int st, int hl) __attribute__((always_inline)) {
-      const int xi = st / (3 * KST), r = st - xi * 3 * KST, kx = r / KST, ks = r - kx * KST;
-      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(b0[kx] ^ (unsigned)((2 * hl + ks) << 6)) +
-                                                               xi * K3W_ROWB + M * 16 * K3P_REC);
-    };
-    constexpr int NSTEP = 12 * KST, DEPTH = 2;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ac[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    f16x8 fb[DEPTH][2];
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      fb[d][0] = frag(d, 0);
-      fb[d][1] = frag(d, 1);
-    }
-    static_for<NSTEP>([&](auto stc) __attribute__((always_inline)) {
-      constexpr int st = decltype(stc)::value, xi = st / (3 * KST), t = st / KST, ks = st % KST;
-      f16x8(&cur)[2] = fb[st % DEPTH];
-      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], ac[xi], 0, 0, 0);  // u_lo*v_hi
-      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], ac[xi], 0, 0, 0);  // u_hi*v_lo
-      ac[xi] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], ac[xi], 0, 0, 0);  // u_hi*v_hi
-      if constexpr (st + DEPTH < NSTEP) {
-        cur[0] = frag(st + DEPTH, 0);
-        cur[1] = frag(st + DEPTH, 1);
-      }
-      hook(stc);
-      __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
-    });
-  };
-  auto no_hook = [](auto) __attribute__((always_inline)) {};
-  // the pair's two output rows (fp32, before bias) of tile M
-  auto out_transform = [&](f32x4& y0, f32x4& y1) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      y0[r] = __fadd_rn(__fadd_rn(acc[0][r], acc[1][r]), acc[2][r]);
-      y1[r] = __fsub_rn(__fsub_rn(acc[1][r], acc[2][r]), acc[3][r]);
-    }
-  };
-  // this lane's granule (chunk_st) of V row xi, record rec, in VB: read as fp32 (hi + lo of
-  // its 4 channels) / write split
-  auto vrec = [&](int xi, int rec) __attribute__((always_inline)) { return vb + xi * K3W_ROWB + opaque(k3p_off(rec, chunk_st)); };
-  auto unpack_v = [&](const u32x4& q) __attribute__((always_inline)) {
-    f16x4 hi, lo;
-    unswap16(q, hi, lo);
-    return unsplit4(hi, lo);
-  };
-  auto write_v = [&](int xi, int rec, const f32x4& v) __attribute__((always_inline)) {
-    range_track(rmax, v);
-    f16x4 hi, lo;
-    split4(v, hi, lo);
-    *(u32x4*)vrec(xi, rec) = swap16_pair(hi, lo);
-  };
-
-  // ---- A epilogue of tile m (conv_a pair (t0, t0 + 1)): VB for conv_b's pair (t0 - 1, t0),
-  // or -- first pair of a segment -- a VB from which the next one recovers (a(t0), a(t0 + 1)).
-  // Pieces 0 .. 6, in order (kK3wIL: spread over the next tile's MFMA steps) ----
-  f32x4 ea0, ea1, ep0, ep1;
-  u32x4 er[3];
-  auto a_epi = [&](int piece, int m, int t0, bool first) __attribute__((always_inline)) {
-    const int x = 16 * m + l16, rec = x + 1;
-    if (piece == 0) {
-      f32x4 y0, y1;
-      out_transform(y0, y1);
-      const bool vx = x < W;
-      const bool v0 = vx && (unsigned)t0 < (unsigned)H, v1 = vx && (unsigned)(t0 + 1) < (unsigned)H;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ea0[r] = v0 ? leaky02(scale_bias(y0[r], scale_a, bias_a[r])) : 0.f;
-        ea1[r] = v1 ? leaky02(scale_bias(y1[r], scale_a, bias_a[r])) : 0.f;
-      }
-    } else if (first) {  // recovers as (p0, p1) = (a0, a1): V1 = V2 = a0, V3 = -a1 (V0 unused)
-      if (piece == 3) write_v(1, rec, ea0);
-      if (piece == 4) write_v(2, rec, ea0);
-      if (piece == 5) write_v(3, rec, -ea1);
-    } else if (piece == 1) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) er[k] = *(const u32x4*)vrec(k + 1, rec);
-    } else if (piece == 2) {
-      const f32x4 o1 = unpack_v(er[0]), o2 = unpack_v(er[1]), o3 = unpack_v(er[2]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ep0[r] = __fmul_rn(__fadd_rn(o1[r], o2[r]), 0.5f);                    // a(t0 - 2)
-        ep1[r] = __fsub_rn(__fmul_rn(__fsub_rn(o1[r], o2[r]), 0.5f), o3[r]);  // a(t0 - 1)
-      }
-    } else {
-      const int xi = piece - 3;
-      f32x4 n;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        n[r] = xi == 0 ? __fsub_rn(ep0[r], ea0[r]) : xi == 1 ? __fadd_rn(ep1[r], ea0[r])
-             : xi == 2 ? __fsub_rn(ea0[r], ep1[r]) : __fsub_rn(ep1[r], ea1[r]);
-      write_v(xi, rec, n);
-    }
-  };
-  constexpr int A_PIECES = 7;
-
-  // ---- B epilogue of tile m (conv_b pair (y, y + 1)): + residual (input rows y, y + 1, loaded
-  // into res[m & 1] when the tile starts), split stores.  Pieces 0 .. 3 ----
-  u32x4 res[2];
-  f32x4 eq0, eq1;
-  auto b_res_load = [&](const __amdgpu_buffer_rsrc_t& rs_in, int m, int y) __attribute__((always_inline)) {
-    const int x = 16 * m + l16;
-    const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
-    const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
-    res[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, v0 ? o0 : kDmaOOR, 0, 0));
-    res[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs_in, v1 ? o0 + (unsigned)(W * K3P_REC) : kDmaOOR, 0, 0));
-  };
-  auto b_epi = [&](int piece, int m, int y, const __amdgpu_buffer_rsrc_t& rs_out) __attribute__((always_inline)) {
-    const int x = 16 * m + l16;
-    const bool vx = x < W, v0 = vx && y < H, v1 = vx && y + 1 < H;
-    if (piece == 0) {
-      f32x4 y0, y1;
-      out_transform(y0, y1);
-      const f32x4 x0 = unpack_v(res[0]), x1 = unpack_v(res[1]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {  // x = x + res (encoder.py:25, decoder.py:29)
-        eq0[r] = __fadd_rn(leaky02(scale_bias(y0[r], scale_b, bias_b[r])), x0[r]);
-        eq1[r] = __fadd_rn(leaky02(scale_bias(y1[r], scale_b, bias_b[r])), x1[r]);
-      }
-    } else {
-      const unsigned o0 = (unsigned)((y * W + x) * K3P_REC + chunk_st * 16);
-      const f32x4 q = piece == 1 ? eq0 : eq1;
-      const bool v = piece == 1 ? v0 : v1;
-      if (v) range_track(rmax, q);
-      f16x4 hi, lo;
-      split4(q, hi, lo);
-      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), rs_out,
-                                             v ? o0 + (piece == 1 ? 0u : (unsigned)(W * K3P_REC)) : kDmaOOR, 0, 0);
-    }
-  };
-  constexpr int B_PIECES = 3;
-
-  // ---- VI for conv_a's pair with input rows d0 = y0 .. d3 = y0 + 3.  Lane (g, l16) of wave w
-  // takes pixel 16 w + l16 (w < MT) and channel chunks g, 4 + g (B-fragment order: conflict-free
-  // reads), each in two halves of 4 channels (half-items k = 2 ks + h); d2 from the prefetch
-  // registers, d3 from the staging row, d0 / d1 recovered from the VI being replaced -- or,
-  // first pair of a segment (FIRST), all four rows from HBM.  Pieces 0 .. 5 per half-item ----
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  u32x4 pf[2][2];  // row d3 of the VI build: [item ks][hi, lo]
-  auto load_item = [&](const __amdgpu_buffer_rsrc_t& rs, int y, int ks, u32x4 (&q)[2]) __attribute__((always_inline)) {
-    const int x = 16 * w + l16;
-    const bool ok = w < MT && (unsigned)y < (unsigned)H && x < W;
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
-      const unsigned off = ok ? (unsigned)((y * W + x) * K3P_REC + (8 * hl + 4 * ks + g) * 16) : kDmaOOR;
-      q[hl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-    }
-  };
-  auto unsplit2x2 = [&](u32x2 hi, u32x2 lo, float (&o)[4]) __attribute__((always_inline)) {
-    o[0] = add_f16_pair<0>(hi[0], lo[0]);
-    o[1] = add_f16_pair<1>(hi[0], lo[0]);
-    o[2] = add_f16_pair<0>(hi[1], lo[1]);
-    o[3] = add_f16_pair<1>(hi[1], lo[1]);
-  };
-  u32x2 bq[4][2];  // raw reads of a half-item: V1', V2', V3', d3 [hi, lo]; then its new V rows
-  auto vi_at = [&](const char* base, int r, int c, int h, int hl) __attribute__((always_inline)) {
-    return base + opaque(k3p_off(r, 8 * hl + c)) + 8 * h;
-  };
-  auto build_piece = [&](int piece, int k) __attribute__((always_inline)) {  // steady state (not FIRST): pieces 0 .. 5
-    const int ks = k >> 1, h = k & 1, c = 4 * ks + g, x = 16 * w + l16, rec = x + 1;
-    auto half_of = [&](const u32x4& q) __attribute__((always_inline)) { return (u32x2){q[2 * h], q[2 * h + 1]}; };
-    if (piece == 0) {
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
-#pragma unroll
-        for (int xi = 1; xi <= 3; ++xi) bq[xi - 1][hl] = *(const u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, hl);
-        bq[3][hl] = *(const u32x2*)vi_at(stg, x, c, h, hl);  // staging record = x (row d2)
-      }
-    } else if (piece == 1) {  // the four new V rows, split in place of the raw reads
-      float v1[4], v2[4], v3[4], d0[4], d1[4], d2[4], d3[4];
-      unsplit2x2(bq[0][0], bq[0][1], v1);
-      unsplit2x2(bq[1][0], bq[1][1], v2);
-      unsplit2x2(bq[2][0], bq[2][1], v3);
-      unsplit2x2(bq[3][0], bq[3][1], d2);                       // staging: row d2
-      unsplit2x2(half_of(pf[ks][0]), half_of(pf[ks][1]), d3);  // registers: row d3
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        d0[e] = __fmul_rn(__fadd_rn(v1[e], v2[e]), 0.5f);                    // d2 of the old pair
-        d1[e] = __fsub_rn(__fmul_rn(__fsub_rn(v1[e], v2[e]), 0.5f), v3[e]);  // its d3
-      }
-#pragma unroll
-      for (int xi = 0; xi < 4; ++xi) {
-        f32x4 n;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          n[e] = xi == 0 ? __fsub_rn(d0[e], d2[e]) : xi == 1 ? __fadd_rn(d1[e], d2[e])
-               : xi == 2 ? __fsub_rn(d2[e], d1[e]) : __fsub_rn(d1[e], d3[e]);
-        range_track(rmax, n);
-        f16x4 hi, lo;
-        split4(n, hi, lo);
-        bq[xi][0] = __builtin_bit_cast(u32x2, hi);
-        bq[xi][1] = __builtin_bit_cast(u32x2, lo);
-      }
-    } else {
-      const int xi = piece - 2;
-      *(u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 0) = bq[xi][0];
-      *(u32x2*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 1) = bq[xi][1];
-    }
-  };
-  constexpr int BUILD_PIECES = 6;
-  auto build_vi_first = [&](const __amdgpu_buffer_rsrc_t& rs, int y0) __attribute__((always_inline)) {  // a segment's prologue
-    if (w >= MT) return;  // wave-uniform
-    const int x = 16 * w + l16, rec = x + 1;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = 4 * ks + g;
-      u32x4 q[4][2];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) load_item(rs, y0 + r, ks, q[r]);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        auto half_of = [&](const u32x4& v) __attribute__((always_inline)) { return (u32x2){v[2 * h], v[2 * h + 1]}; };
-        float d[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) unsplit2x2(half_of(q[r][0]), half_of(q[r][1]), d[r]);
-#pragma unroll
-        for (int xi = 0; xi < 4; ++xi) {
-          f32x4 n;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            n[e] = xi == 0 ? __fsub_rn(d[0][e], d[2][e]) : xi == 1 ? __fadd_rn(d[1][e], d[2][e])
-                 : xi == 2 ? __fsub_rn(d[2][e], d[1][e]) : __fsub_rn(d[1][e], d[3][e]);
-          range_track(rmax, n);
-          f16x4 hi, lo;
-          split4(n, hi, lo);
-          *(f16x4*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 0) = hi;
-          *(f16x4*)vi_at(vi + xi * K3W_ROWB, rec, c, h, 1) = lo;
-        }
-      }
-    }
-  };
-
-  // the staging DMA of input row y (records 0 .. 63, chunk k of record r in slot k ^ (2r & 15))
-  auto dma_stage = [&](const __amdgpu_buffer_rsrc_t& rs, int y) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = w; k < 16; k += 4) {  // 16 pieces of 1 KB
-      const int q = 64 * k + lane, rec = q >> 4, ch = (q & 15) ^ ((2 * rec) & 15);
-      const bool ok = (unsigned)y < (unsigned)H && rec < W;
-      dma16_buf(rs, ok ? (unsigned)((y * W + rec) * K3P_REC + ch * 16) : kDmaOOR, stg + k * 1024);
-    }
-  };
-
-  // A-step: conv_a pair (t0, t0 + 1) from VI, its epilogue into VB
-  auto a_step = [&](int t0, auto first_c) __attribute__((always_inline)) {
-    constexpr bool first = decltype(first_c)::value;
-    static_for<MT>([&](auto mc) __attribute__((always_inline)) {
-      constexpr int m = decltype(mc)::value;
-      if constexpr (kK3wIL && m > 0) {  // tile m - 1's epilogue inside tile m's stream
-        mfma_tile(vi, wa, mc, [&](auto stc) __attribute__((always_inline)) {
-          constexpr int st = decltype(stc)::value;
-          if constexpr (st == -1) a_epi(0, m - 1, t0, first);  // the sums, before acc restarts
-          if constexpr (st >= 0 && st % 3 == 0 && st / 3 + 1 < A_PIECES) a_epi(st / 3 + 1, m - 1, t0, first);
-        });
-      } else {
-        mfma_tile(vi, wa, mc, no_hook);
-        if constexpr (!kK3wIL) static_for<A_PIECES>([&](auto pc) __attribute__((always_inline)) { a_epi(decltype(pc)::value, m, t0, first); });
-      }
-    });
-    if constexpr (kK3wIL) static_for<A_PIECES>([&](auto pc) __attribute__((always_inline)) { a_epi(decltype(pc)::value, MT - 1, t0, first); });
-  };
-  // B-step: conv_b pair (y, y + 1) from VB (+ residual, stores); with `build`, the VI of the
-  // next conv_a pair (in place, half-item m in tile m's stream when MT = 4)
-  auto b_step = [&](const __amdgpu_buffer_rsrc_t& rs_in, const __amdgpu_buffer_rsrc_t& rs_out, int y, auto conv_c,
-                    auto build_c) __attribute__((always_inline)) {
-    constexpr bool conv = decltype(conv_c)::value, build = decltype(build_c)::value;
-    constexpr bool IL_BUILD = kK3wIL && MT == 4;
-    if constexpr (conv) {
-      static_for<MT>([&](auto mc) __attribute__((always_inline)) {
-        constexpr int m = decltype(mc)::value;
-        if constexpr (kK3wIL) {
-          mfma_tile(vb, wb, mc, [&](auto stc) __attribute__((always_inline)) {
-            constexpr int st = decltype(stc)::value;
-            if constexpr (st == -1) {  // the previous tile's sums + residual, then this tile's residual loads
-              if constexpr (m > 0) b_epi(0, m - 1, y, rs_out);
-              b_res_load(rs_in, m, y);
-            }
-            if constexpr (m > 0 && st >= 0 && st % 2 == 0 && st / 2 + 1 < B_PIECES) b_epi(st / 2 + 1, m - 1, y, rs_out);
-            if constexpr (build && IL_BUILD && st >= 6 && (st - 6) % 3 == 0 && (st - 6) / 3 < BUILD_PIECES)
-              build_piece((st - 6) / 3, m);
-          });
-        } else {
-          b_res_load(rs_in, m, y);
-          mfma_tile(vb, wb, mc, no_hook);
-          static_for<B_PIECES>([&](auto pc) __attribute__((always_inline)) { b_epi(decltype(pc)::value, m, y, rs_out); });
-        }
-      });
-      if constexpr (kK3wIL) static_for<B_PIECES>([&](auto pc) __attribute__((always_inline)) { b_epi(decltype(pc)::value, MT - 1, y, rs_out); });
-    }
-    if constexpr (build && (!IL_BUILD || !conv))
-      if (w < MT)
-        static_for<4>([&](auto k) __attribute__((always_inline)) {
-        static_for<BUILD_PIECES>([&](auto pc) __attribute__((always_inline)) { build_piece(decltype(pc)::value, decltype(k)::value); });
-      });
-  };
-
-  for (long long gs = g0; gs < g1;) {
-    const int p = (int)(gs / hp);
-    const int j0 = (int)(gs - (long long)p * hp), j1 = (int)min((long long)hp, g1 - (long long)p * hp);
-    const int K = j1 - j0, r0 = 2 * j0;
-    gs = (long long)p * hp + j1;
-    const int m_item = p >= a.nimg ? 1 : 0;
-    if (m_item != model) {  // block-uniform: items of one model are consecutive
-      model = m_item;
-      load_weights(model);
-    }
-    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
-    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)a.out_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
-    // prologue: VI of P_0 (input rows r0 - 2 .. r0 + 1); the previous segment's last conv_b
-    // pair has read VB and its stores are in flight
-    build_vi_first(rs_in, r0 - 2);
-    lds_reads_done();
-    stage_barrier();
-    // step i (0 <= i <= K), the first and last peeled so that every branch of a step is resolved
-    // at compile time (none inside the MFMA streams)
-    auto step = [&](int i, auto first_c, auto conv_c, auto build_c) __attribute__((always_inline)) {
-      constexpr bool build = decltype(build_c)::value;
-      // A: conv_a pair P_i from VI -> VB (Q_{i-1}); the staging DMA of the next VI build's row
-      // d2 is issued first so it lands during the MFMAs
-      if constexpr (build) dma_stage(rs_in, r0 + 2 * i + 2);
-      a_step(r0 + 2 * i - 1, first_c);
-      dma_wait_all();  // this wave's staging pieces (other waves' lanes read them)
-      lds_reads_done();
-      stage_barrier();  // VB of Q_{i-1} and the staging row complete; every wave's VI reads done
-      // B: conv_b pair Q_{i-1} from VB, and the VI of P_{i+1} (in place; its row d3 loaded now,
-      // used late in the step)
-      if constexpr (build) {
-        load_item(rs_in, r0 + 2 * i + 3, 0, pf[0]);
-        load_item(rs_in, r0 + 2 * i + 3, 1, pf[1]);
-      }
-      b_step(rs_in, rs_out, r0 + 2 * i - 2, conv_c, build_c);
-      lds_reads_done();
-      stage_barrier();  // VI of P_{i+1} complete; every wave's VB reads done
-    };
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    step(0, T_{}, F_{}, T_{});
-    for (int i = 1; i < K; ++i) step(i, F_{}, T_{}, T_{});
-    step(K, F_{}, T_{}, F_{});
-  }
-  range_report(a.rg, rmax);
-}
-
-bool k3wino_supported(int H, int W) {
-  return H > 0 && W > 0 && W <= K3P_MAX_W && (long long)H * W * K3P_REC < (1LL << 31);
-}
+// (Round 4 built the pair on Winograd F(2,3) along y -- 2/3 of the products, both layers' U
+// kernels resident in one wave per SIMD -- and measured it 16 % slower than this direct pair:
+// with one wave per SIMD nothing hides the transform VALU; removed in round 5,
+// see DESIGN section 9 for why a two-wave form does not fit the 160 KB of LDS either.)
 
 // ------------------------------------------------------------------------------------
 // conv1 (1 -> 32, k5 s2) with the RGB -> YCbCr front end fused (encoder.py:39-41,
@@ -5380,28 +4796,6 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// The fused k3 residual pair: persistent blocks (one per CU), each a contiguous range of the
-// planes' rows (planes in order, so a block reloads its weights only when the model changes).
-hipError_t launch_k3wino_x3(const ConvArgs& a0, hipStream_t st) {
-  ConvArgs a = a0;
-  if (!k3wino_supported(a.H, a.W) || a.OH != a.H || a.OW != a.W || !a.wxw || !a.wxw2 || !a.bias2 ||
-      a.P != 3 * a.nimg)
-    return hipErrorInvalidValue;
-  const long long pairs = (long long)a.P * ((a.H + 1) / 2);
-  if (pairs == 0) return hipSuccess;
-  // one block per CU, at least 2 row pairs per block (a block's fixed cost: the prologue VI
-  // build from four HBM rows and one recomputed conv_a row)
-  const int grid = (int)std::max(1LL, std::min<long long>((pairs + 1) / 2, device_cus()));
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a); };
-  switch ((a.W + 15) / 16) {
-    case 1: go(conv_k3wino_kernel<1>); break;
-    case 2: go(conv_k3wino_kernel<2>); break;
-    case 3: go(conv_k3wino_kernel<3>); break;
-    default: go(conv_k3wino_kernel<4>); break;
-  }
-  return hipGetLastError();
-}
-
 // Block row ranges of the fused pair by pipeline steps.  A block pays ~3 fill steps per segment
 // (the part of its range inside one (plane, strip) column of H rows) on top of one step per row:
 // equal-row ranges give the blocks that straddle a plane boundary 2 segments (config 2: 48 rows
@@ -5738,15 +5132,6 @@ static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = by;
   a.ws_blk[2] = by + bc;
-  // NIC_D1M=1: one block group over both models' tiles (every block 12 tiles at config 2
-  // instead of 13 for a few Y blocks) -- measured slower, the mid-walk weight reload costs more
-  // than the tail: dconv1 0.0604-0.0608 vs 0.0555-0.0567 ms (3 rounds, profiles/r4_ab_logs.txt)
-  static const bool mixed = [] {
-    const char* e = getenv("NIC_D1M");
-    return e && e[0] == '1';
-  }();
-  a.d1_mixed = mixed ? 1 : 0;
-  if (mixed) a.ws_blk[1] = a.ws_blk[2] = (int)std::min<long long>(nt, target);  // one group: gi = 0, nb = grid
   hipLaunchKernelGGL(dconv1_all_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   return hipGetLastError();
 }

@@ -27,8 +27,8 @@ from test_gpu_parity import PREQUANT_ATOL, check_codes, check_recon  # noqa: E40
 def main():
     ws_off = os.environ.get("NIC_WS") == "0"
     assert (ws_off or os.environ.get("NIC_D8") in ("tile", "strip") or os.environ.get("NIC_D8G") == "l"
-            or os.environ.get("NIC_K3P") in ("0", "w") or os.environ.get("NIC_K3P_SK") == "0"
-            or os.environ.get("NIC_K3P_BAL") == "0" or os.environ.get("NIC_D1M") == "1"
+            or os.environ.get("NIC_K3P") == "0" or os.environ.get("NIC_K3P_SK") == "0"
+            or os.environ.get("NIC_K3P_BAL") == "0"
             or os.environ.get("NIC_D1") in ("x", "p"))
     c = Codec(0, precision="f16x3")
     c.set_weights(W.seeded_weights(0, init="spread"))

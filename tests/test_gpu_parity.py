@@ -389,23 +389,9 @@ def test_pack_unpack_bit_exact(codecs):
     np.testing.assert_array_equal(c.unpack(p).cpu().numpy(), z)
 
 
-@pytest.mark.parametrize("slots", ["1", "2"])
-def test_numpy_surface_concurrent_chunks(slots, weights_spread, tmp_path):
+def test_numpy_surface_chunks(weights_spread):
     """The host pipeline on a config-2 batch (64 x 256^2) with ragged chunkings gives the device
-    path's bytes exactly -- with one compute stream (default) and with NIC_HOST_SLOTS=2 (odd
-    chunks on a second stream with the ctx's second pass slot: own activation regions and
-    range-guard words, two chunk passes in flight; child process, read at library load)."""
-    if slots == "2":
-        import subprocess
-        code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import torch; "
-                "import test_gpu_parity as T; "
-                "from neural_network_image_compression_amd import weights as W; "
-                "T._surface_check(W.seeded_weights(0, init='spread')); print('SLOTS-OK')"
-                % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__))))
-        out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, NIC_HOST_SLOTS="2"),
-                             capture_output=True, text=True, timeout=300)
-        assert out.returncode == 0 and "SLOTS-OK" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
-        return
+    path's bytes exactly."""
     _surface_check(weights_spread)
 
 
@@ -508,14 +494,13 @@ def test_f16_range_guard(golden, weights_spread):
     range_guard_contract(golden, weights_spread)
 
 
-@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "1"}, {"NIC_HOST_SLOTS": "2"}],
-                         ids=["per-layer", "cooperative", "host-two-slots"])
+@pytest.mark.parametrize("switches", [{"NIC_CHAIN": "0"}, {"NIC_COOP": "1"}],
+                         ids=["per-layer", "cooperative"])
 def test_f16_range_guard_rerun_variants(switches):
     """The same contract with the gated re-run as one launch per layer (NIC_CHAIN=0: every
     fp32 kernel checks the gate itself), as a cooperative chained launch (NIC_COOP=1; the
-    default is a plain launch, see launch_fp32_chain), and with the host surface's odd chunks
-    on the second pass slot (NIC_HOST_SLOTS=2: their trips land in its own guard words, summed
-    by nic_range_trips); child process, the switches are read when libnic.so loads."""
+    default is a plain launch, see launch_fp32_chain); child process, the switches are read when
+    libnic.so loads."""
     import os
     import subprocess
     import sys
@@ -669,9 +654,9 @@ def _alt_child(tmp_path, switches, tag):
 
 @pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
                                       {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}, {"NIC_K3P_BAL": "0"},
-                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}, {"NIC_D1M": "1"}],
+                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}],
                          ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "k3-equal-rows",
-                              "dconv1-tile", "dconv1-perphase", "dconv1-mixed-groups"])
+                              "dconv1-tile", "dconv1-perphase"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
     NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the k3 layers
@@ -680,11 +665,11 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     golden contract too; they run in a child process because the switches are read when the
     library loads."""
     dump = _alt_child(tmp_path, switches, "v")
-    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_D1M": "1"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
+    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
                     {"NIC_K3P_BAL": "0"}):
         # the LDS-staged gather sums the same projections in the same order as the direct one;
         # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue, with
-        # one block group per model or one over both models (NIC_D1M=1); the
+        # one block group per model; the
         # default (direct 9-tap) fused k3 residual pair runs the same chains and epilogues as
         # the two weight-stationary launches, in either step order and under either block range
         # split (a range boundary inside a plane recomputes the same conv_a row): bit-identical
@@ -698,35 +683,3 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
         with np.load(dump) as other:
             for k, v in mine.items():
                 np.testing.assert_array_equal(v.cpu().numpy(), other[k], err_msg=k)
-
-
-def test_k3_wino_against_direct_pair(tmp_path, weights_spread):
-    """The Winograd F(2,3)-along-y k3 pair (NIC_K3P=w, planes up to 64 columns; child process)
-    against the default direct 9-tap pair on the alt_kernels_check cases: codes and
-    reconstructions within the oracle contract of each other, pre-quant latents within
-    PREQUANT_ATOL (both are within it of the float64 oracle); the max differences are printed."""
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from alt_kernels_check import alt_cases
-
-    from neural_network_image_compression_amd.codec import Codec
-    ref = _alt_child(tmp_path, {"NIC_K3P": "w"}, "w")
-    c = Codec(0, precision="f16x3")
-    c.set_weights(weights_spread)
-    mine = {k: v.cpu().numpy() for k, v in alt_cases(c).items()}
-    worst = {}
-    with np.load(ref) as b:
-        for k in b.files:
-            if k.endswith("_f") or k.endswith("_z"):
-                continue
-            d = np.abs(mine[k].astype(int) - b[k].astype(int)).max()
-            assert d <= 1, (k, d)
-            worst[k] = int(d)
-        for k in b.files:
-            if k.endswith("_f"):
-                d = float(np.abs(mine[k] - b[k]).max())
-                assert d <= PREQUANT_ATOL, (k, d)
-                worst[k] = d
-                z = k[:-2] + "_z"
-                flips = np.abs(mine[z].astype(int) - b[z].astype(int))
-                assert flips.max() <= 1 and flips.mean() <= 1e-3, (z, flips.max(), flips.mean())
-    print("wino vs direct:", worst)

@@ -26,7 +26,7 @@ LAYER_OF = [  # kernel-name pattern -> bench layer name (order matters: first ma
     (r"conv_ws_kernel<64, 64, 8, 8, true, false", "k3_resid"), (r"conv_ws_kernel<64, 64, 8, 8, false, false", "k3"),
     (r"<64, 64, 3, 1, false.*true>", "k3_resid"), (r"<64, 64, 3, 1, false.*false>", "k3"),
     (r"latent_hist", "hist"), (r"hist_entropy", "entropy"), (r"conv_k3pair_kernel", "k3_pair"),
-    (r"conv_k3wino_kernel", "k3_pair"), (r"dconv1_all_kernel", "dconv1"),
+    (r"dconv1_all_kernel", "dconv1"),
     (r"colour_split", "colour"), (r"fp32_chain", "fp32_chain"), (r"dconv1_ws_kernel", "dconv1"),
 ]
 
