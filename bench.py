@@ -216,6 +216,51 @@ def parity_sample(codec, x0, weights):
     return out
 
 
+def host_box_rates(xh, enc, dec, reps):
+    """What the host-array surface depends on besides the device: the CPUs this
+    process may run on, single-thread pageable -> pinned memcpy of the batch, pinned H2D / D2H
+    copies of it, and the encode / decode calls' own medians -- so boxes can be compared."""
+    import torch
+    nbytes = xh.nbytes
+    pin = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    pin_np = pin.numpy()
+    src = xh.reshape(-1)
+    dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+
+    def best(fn, n=7):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    def h2d():
+        dev.copy_(pin, non_blocking=True)
+        torch.cuda.synchronize()
+
+    def d2h():
+        pin.copy_(dev, non_blocking=True)
+        torch.cuda.synchronize()
+
+    t_cp = best(lambda: np.copyto(pin_np, src))
+    t_h2d, t_d2h = best(h2d), best(d2h)
+    te, td = [], []
+    z = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        z = enc(xh)
+        t1 = time.perf_counter()
+        dec(z)
+        te.append(t1 - t0)
+        td.append(time.perf_counter() - t1)
+    return {"cpus_allowed": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(),
+            "pageable_to_pinned_gbps": round(nbytes / t_cp / 1e9, 1),
+            "h2d_pinned_gbps": round(nbytes / t_h2d / 1e9, 1), "d2h_pinned_gbps": round(nbytes / t_d2h / 1e9, 1),
+            "bytes": int(nbytes), "encode_call_ms_median": round(float(np.median(te)) * 1e3, 3),
+            "decode_call_ms_median": round(float(np.median(td)) * 1e3, 3)}
+
+
 def bench_weights(kind: str):
     """The timed workload's weights: the seeded 'spread' init (default), or the committed
     round-4 trained codec (entropy_loss_coef 0.01) for the informational operand comparison."""
@@ -447,6 +492,7 @@ def main():
             dec(enc(xh))
         hp = (time.perf_counter() - t0) / reps
         host_path = {"mp_per_s": round(B * H * W / 1e6 / hp, 1), "ms_per_batch": round(hp * 1e3, 3),
+                     "box": host_box_rates(xh, enc, dec, reps),
                      "path": "Encoder()(numpy) -> Decoder()(numpy) via nic_encode_host / nic_decode_host: "
                              f"{Encoder.host_chunks} ramped chunks per call, H2D / device pass / D2H on three "
                              "HIP streams; pageable input staged through pinned memory, results returned "

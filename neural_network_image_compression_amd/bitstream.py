@@ -161,23 +161,75 @@ def feed_batch(model, x: np.ndarray, filenames: Sequence[str], output_dir: str, 
     return [pool.submit(save_imgs, imgs, output_dir, list(filenames), png_threads)]
 
 
+def list_dataset(dataset_path: str) -> List[str]:
+    """utils.py:92-94: the sorted directory entries with an image extension."""
+    return [fn for fn in sorted(os.listdir(dataset_path)) if fn.split(".")[-1] in IMAGE_EXTS]
+
+
+def _read_one(path: str):
+    from PIL import Image
+
+    with Image.open(path) as im:
+        return np.array(im)
+
+
+def _host_threads() -> int:
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:  # pragma: no cover
+        return max(1, os.cpu_count() or 1)
+
+
 def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, in_cshape: int,
-              batch_size: int = 4, workers: int = 0) -> None:
-    """utils.py:46-62.  ``workers`` > 0: PNG encoding (``save_img``, ~74 ms per 256^2 latent
-    with optimize=True on one core) runs on that many host threads, overlapped with the
-    device work of the following batches; the files written are byte-identical."""
+              batch_size: int = 64, workers=None) -> None:
+    """utils.py:46-62: every colour image of ``dataset_path`` (sorted; read_dataset's filter)
+    through the codec into ``output_dir``, one PNG per image named after its source.
+
+    ``workers=0`` is the reference's serial loop (read everything, then batches of
+    ``batch_size`` -- the reference's 4 -- each run and saved inline).  Otherwise (default) a
+    pipeline over the host cores: images are decoded by a reader pool in file order, consecutive
+    equal-shaped images are fed to the device ``batch_size`` (64) at a time, and each batch's PNG
+    files are encoded natively on ``workers`` threads (default: every CPU this process may use,
+    at most 16) while the next batches are read and run.  Every image's output depends on that
+    image alone (the kernels are batch-invariant), so the files are byte-identical either way."""
     os.makedirs(output_dir, exist_ok=True)
     model.load(checkpoint_path)
-    imgs, names = read_dataset(dataset_path)
-    if workers <= 0:
+    if workers is not None and workers <= 0:
+        imgs, names = read_dataset(dataset_path)
         for i, j in _batches([a.shape for a in imgs], batch_size):
             feed_batch(model, np.stack(imgs[i:j]), names[i:j], output_dir, in_cshape)
         return
     from concurrent.futures import ThreadPoolExecutor
 
-    with ThreadPoolExecutor(max_workers=workers) as pool:
-        futures = []
-        for i, j in _batches([a.shape for a in imgs], batch_size):
-            futures += feed_batch(model, np.stack(imgs[i:j]), names[i:j], output_dir, in_cshape, pool=pool)
+    threads = _host_threads()
+    png_threads = int(workers) if workers else min(16, threads)
+    files = list_dataset(dataset_path)
+    with ThreadPoolExecutor(max_workers=min(8, threads)) as readers, ThreadPoolExecutor(max_workers=1) as writer:
+        futures, batch, names, depth = [], [], [], 4 * max(1, batch_size)
+        pending = [readers.submit(_read_one, os.path.join(dataset_path, fn)) for fn in files[:depth]]
+
+        def flush():
+            nonlocal futures
+            if batch:
+                futures += feed_batch(model, np.stack(batch), list(names), output_dir, in_cshape, pool=writer,
+                                      png_threads=png_threads)
+                batch.clear()
+                names.clear()
+            for f in [f for f in futures if f.done()]:
+                f.result()  # re-raise a write error early
+            futures = [f for f in futures if not f.done()]
+
+        for k, fn in enumerate(files):
+            a = pending[k].result()
+            if k + depth < len(files):  # keep `depth` decodes in flight ahead of the device
+                pending.append(readers.submit(_read_one, os.path.join(dataset_path, files[k + depth])))
+            pending[k] = None
+            if a.ndim != 3:  # read_dataset keeps colour (3-D) images only
+                continue
+            if batch and (a.shape != batch[0].shape or len(batch) >= batch_size):
+                flush()
+            batch.append(a.astype(np.uint8, copy=False))
+            names.append(".".join(fn.split(".")[:-1]))
+        flush()
         for f in futures:
             f.result()  # re-raise any write error

@@ -374,9 +374,10 @@ class Encoder(ProClass):
             raise ValueError(f"Encoder: expected shape (N,H,W,3), got {a.shape}")
         return self.codec.encode_host(a, self.host_chunks)
 
-    def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
+    def compress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 64, workers=None) -> None:
         """encoder.py:49-51: every image in ``dataset_path`` -> ``dataset_path + '_compressed'``.
-        ``workers``: host threads for the PNG writes (0 = inline, as the reference)."""
+        Pipelined over the host cores in batches of ``batch_size`` (bitstream.use_model);
+        ``workers=0, batch_size=4`` is the reference's serial loop (same files)."""
         from .bitstream import use_model
 
         use_model(self, dataset_path, checkpoint_path, dataset_path + "_compressed", in_cshape=3,
@@ -396,8 +397,9 @@ class Decoder(ProClass):
             raise ValueError(f"Decoder: expected shape (N,h,w,96), got {a.shape}")
         return self.codec.decode_host(a, self.host_chunks)
 
-    def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 4, workers: int = 0) -> None:
-        """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``."""
+    def uncompress(self, dataset_path: str, checkpoint_path: str, batch_size: int = 64, workers=None) -> None:
+        """decoder.py:50-52: packed PNGs in ``dataset_path`` -> ``dataset_path.replace('compressed','uncompressed')``.
+        Pipelined as compress (``workers=0, batch_size=4``: the reference's serial loop)."""
         from .bitstream import use_model
 
         use_model(self, dataset_path, checkpoint_path, dataset_path.replace("compressed", "uncompressed"),

@@ -1,10 +1,9 @@
 """Directory throughput of the reference's file-level API: Encoder.compress /
 Decoder.uncompress (encoder.py:49-51, decoder.py:50-52, utils.py:30-62, 85-87) on a directory of
 256^2 RGB PNG tiles cut from kodim21 (the reference's validation image; 6 tiles, flipped and
-shifted into `--images` distinct ones).  Reports images/s and MP/s per surface and PNG writer:
-
-  native  -- bitstream.save_imgs: nic_png_encode on 16 host threads (Pillow-identical bytes)
-  pillow  -- Pillow optimize=True per image on `--workers` Python threads (round 3's writer)
+shifted into `--images` distinct ones).  Reports images/s and MP/s per driver mode (the reference's serial loop, round 4's threaded
+writes, round 5's pipeline) on the kodim21 tiles and on data/imagenet_patches_1k, and whether
+every mode wrote the same bytes.
 
 Output: one JSON line.  Needs the GPU (the codec) and the built library."""
 import argparse
@@ -42,16 +41,41 @@ def tiles(n):
     return out
 
 
+def run_modes(enc, dec, tmp, ds, ck, n, px, modes, repeat):
+    """Best-of-`repeat` compress / uncompress wall time per driver mode (after a warm-up round)."""
+    res, files = {}, {}
+    for name, kw in modes:
+        best = {}
+        for r in range(repeat + 1):  # the first round warms up (HIP modules, page cache)
+            for d in (os.path.basename(ds) + "_compressed", os.path.basename(ds) + "_uncompressed"):
+                shutil.rmtree(os.path.join(tmp, d), ignore_errors=True)
+            t0 = time.perf_counter()
+            enc.compress(ds, os.path.join(ck, "encoder"), **kw)
+            t1 = time.perf_counter()
+            dec.uncompress(ds + "_compressed", os.path.join(ck, "decoder"), **kw)
+            t2 = time.perf_counter()
+            if r:
+                best["compress_s"] = min(best.get("compress_s", 1e9), t1 - t0)
+                best["uncompress_s"] = min(best.get("uncompress_s", 1e9), t2 - t1)
+        out = {k: round(v, 4) for k, v in best.items()}
+        out.update({"compress_img_s": round(n / best["compress_s"], 1), "uncompress_img_s": round(n / best["uncompress_s"], 1),
+                    "compress_MP_s": round(n * px / 1e6 / best["compress_s"], 2),
+                    "uncompress_MP_s": round(n * px / 1e6 / best["uncompress_s"], 2), "args": kw})
+        res[name] = out
+        files[name] = {d: {f: open(os.path.join(ds + d, f), "rb").read() for f in sorted(os.listdir(ds + d))}
+                       for d in ("_compressed", "_uncompressed")}
+    same = all(files[k] == files[modes[0][0]] for k in files)
+    return res, same
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=192)
-    ap.add_argument("--batch", type=int, default=4, help="utils.py:53 batches of 4")
-    ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--imagenet", default=os.path.join(ROOT, "data", "imagenet_patches_1k"))
     args = ap.parse_args()
     from PIL import Image
 
-    from neural_network_image_compression_amd import bitstream as B
     from neural_network_image_compression_amd import weights as W
     from neural_network_image_compression_amd.codec import Decoder, Encoder
 
@@ -61,51 +85,27 @@ def main():
         os.makedirs(ds)
         for i, t in enumerate(tiles(args.images)):
             Image.fromarray(t).save(os.path.join(ds, f"t{i:05d}.png"))
+        ck = os.path.join(tmp, "ck")
         w = W.seeded_weights(0, init="spread")
-        W.save(w, os.path.join(tmp, "ck", "encoder"), "encoder")
-        W.save(w, os.path.join(tmp, "ck", "decoder"), "decoder")
+        W.save(w, os.path.join(ck, "encoder"), "encoder")
+        W.save(w, os.path.join(ck, "decoder"), "decoder")
         enc, dec = Encoder(0), Decoder(0)
-        native_save = B.save_imgs
-
-        def pillow_save(imgs, output_dir, filenames, threads=16):  # round 3's per-image Pillow writer
-            paths = []
-            for a, name in zip(imgs, filenames):
-                p = os.path.join(output_dir, name + ".png")
-                with open(p, "wb") as f:
-                    f.write(B.png_bytes(np.asarray(a, np.uint8)))
-                paths.append(p)
-            return paths
-
-        res = {}
-        for writer, fn in (("native", native_save), ("pillow", pillow_save)):
-            B.save_imgs = fn
-            best = {}
-            for r in range(args.repeat + 1):  # first round warms up (HIP modules, page cache)
-                for d in ("tiles_compressed", "tiles_uncompressed"):
-                    shutil.rmtree(os.path.join(tmp, d), ignore_errors=True)
-                t0 = time.perf_counter()
-                enc.compress(ds, os.path.join(tmp, "ck", "encoder"), batch_size=args.batch, workers=args.workers)
-                t1 = time.perf_counter()
-                dec.uncompress(os.path.join(tmp, "tiles_compressed"), os.path.join(tmp, "ck", "decoder"),
-                               batch_size=args.batch, workers=args.workers)
-                t2 = time.perf_counter()
-                if r:
-                    best["compress_s"] = min(best.get("compress_s", 1e9), t1 - t0)
-                    best["uncompress_s"] = min(best.get("uncompress_s", 1e9), t2 - t1)
-            n = args.images
-            res[writer] = {k: round(v, 4) for k, v in best.items()}
-            res[writer].update({"compress_img_s": round(n / best["compress_s"], 1),
-                                "uncompress_img_s": round(n / best["uncompress_s"], 1),
-                                "compress_MP_s": round(n * 65536 / 1e6 / best["compress_s"], 2),
-                                "uncompress_MP_s": round(n * 65536 / 1e6 / best["uncompress_s"], 2)})
-            if writer == "native":
-                files = {f: open(os.path.join(tmp, "tiles_compressed", f), "rb").read()
-                         for f in sorted(os.listdir(os.path.join(tmp, "tiles_compressed")))[:8]}
-        B.save_imgs = native_save
-        same = all(open(os.path.join(tmp, "tiles_compressed", f), "rb").read() == b for f, b in files.items())
-        print(json.dumps({"tool": "compress_bench", "images": args.images, "tile": "256x256x3 kodim21 tiles",
-                          "batch": args.batch, "workers": args.workers, "writers": res,
-                          "native_equals_pillow_files": same}), flush=True)
+        # the reference's serial loop (utils.py:46-62: batches of 4, each saved inline), round 4's
+        # default (batches of 4, PNG writes on 8 threads behind the device), round 5's pipeline
+        modes = [("serial_b4", {"batch_size": 4, "workers": 0}), ("r4_b4_w8", {"batch_size": 4, "workers": 8}),
+                 ("pipeline_b64", {})]
+        out = {"tool": "compress_bench", "host_cpus": len(os.sched_getaffinity(0))}
+        res, same = run_modes(enc, dec, tmp, ds, ck, args.images, 65536, modes, args.repeat)
+        out["kodim21_tiles"] = {"images": args.images, "tile": "256x256x3 kodim21 tiles", "modes": res,
+                                "files_identical_across_modes": same}
+        if os.path.isdir(args.imagenet):
+            inet = os.path.join(tmp, "inet")
+            shutil.copytree(args.imagenet, inet)
+            n = len([f for f in os.listdir(inet) if f.endswith(".jpg")])
+            res, same = run_modes(enc, dec, tmp, inet, ck, n, 128 * 128, modes, args.repeat)
+            out["imagenet_patches_1k"] = {"images": n, "tile": "128x128x3 JPEG patches", "modes": res,
+                                          "files_identical_across_modes": same}
+        print(json.dumps(out), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
