@@ -628,16 +628,33 @@ def test_compress_uncompress_directory(tmp_path, codecs, weights_spread, golden)
     rec = np.array(Image.open(tmp_path / "kodak_uncompressed" / "img1.png"))
     np.testing.assert_array_equal(rec, codecs["spread"].decode(_dev(z)).cpu().numpy()[0])
     assert (tmp_path / "kodak_uncompressed" / "img1.png").read_bytes() == png_bytes(rec)
-    # threaded PNG writes (workers > 0) produce byte-identical files
+    # the pipelined driver (default: reader pool, device batches, native PNG threads) and the
+    # reference's serial loop (workers=0, batches of 4) write the same files; a greyscale image
+    # is skipped (read_dataset keeps 3-D arrays), an odd-sized one breaks the batch, other
+    # files are ignored
+    import shutil
     ds2 = tmp_path / "thr"
     ds2.mkdir()
     for i in range(3):
         Image.fromarray(g["x"][i]).save(ds2 / f"img{i}.png")
+    Image.fromarray(np.ascontiguousarray(g["x"][0][:200, :120])).save(ds2 / "img1b.png")
+    Image.fromarray(np.ascontiguousarray(g["x"][2][..., 1])).save(ds2 / "grey.png")
+    (ds2 / "notes.txt").write_text("not an image")
+    shutil.copytree(ds2, tmp_path / "ser")
     enc.compress(str(ds2), ck, batch_size=2, workers=3)
-    dec.uncompress(str(tmp_path / "thr_compressed"), str(tmp_path / "ckpt" / "decoder"), workers=2)
+    enc.compress(str(tmp_path / "ser"), ck, batch_size=4, workers=0)
+    dec.uncompress(str(tmp_path / "thr_compressed"), str(tmp_path / "ckpt" / "decoder"), batch_size=3)
+    dec.uncompress(str(tmp_path / "ser_compressed"), str(tmp_path / "ckpt" / "decoder"), workers=0)
+    for a, b in (("thr_compressed", "ser_compressed"), ("thr_uncompressed", "ser_uncompressed")):
+        names = sorted(os.listdir(tmp_path / a))
+        assert names == sorted(os.listdir(tmp_path / b)) == ["img0.png", "img1.png", "img1b.png", "img2.png"]
+        for n in names:
+            assert (tmp_path / a / n).read_bytes() == (tmp_path / b / n).read_bytes(), (a, n)
     for i in range(3):
         for a, b in (("kodak_compressed", "thr_compressed"), ("kodak_uncompressed", "thr_uncompressed")):
             assert (tmp_path / a / f"img{i}.png").read_bytes() == (tmp_path / b / f"img{i}.png").read_bytes()
+    z1b = codecs["spread"].encode(_dev(np.ascontiguousarray(g["x"][0:1, :200, :120]))).cpu().numpy()
+    assert (tmp_path / "thr_compressed" / "img1b.png").read_bytes() == png_bytes(O.pack_latent(z1b)[0])
 
 
 def _alt_child(tmp_path, switches, tag):
@@ -668,8 +685,7 @@ def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
     if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
                     {"NIC_K3P_BAL": "0"}):
         # the LDS-staged gather sums the same projections in the same order as the direct one;
-        # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue, with
-        # one block group per model; the
+        # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue; the
         # default (direct 9-tap) fused k3 residual pair runs the same chains and epilogues as
         # the two weight-stationary launches, in either step order and under either block range
         # split (a range boundary inside a plane recomputes the same conv_a row): bit-identical
