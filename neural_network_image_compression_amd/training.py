@@ -405,11 +405,13 @@ class Training:
 
     def __call__(self, x: np.ndarray, x_val_path: Optional[str], max_epochs: int, batch_size: int,
                  entropy_loss_coef: float, verbose: bool = True,
-                 epoch_samples: Optional[int] = None) -> List[Dict[str, object]]:
+                 epoch_samples: Optional[int] = None, coef_step: float = 0.01) -> List[Dict[str, object]]:
         """training.py:53-165: epochs over shuffled batches of the u8 array x (N,H,W,3).
         ``epoch_samples``: the epoch length in images when x is a subset of the reference's
         training set (each epoch then walks that many images over reshuffled passes of x, so
-        the per-epoch coefficient schedule keeps the reference's pace); None = one pass."""
+        the per-epoch coefficient schedule keeps the reference's pace); None = one pass.
+        ``coef_step``: the coefficient's increment after every epoch (training.py:165: 0.01;
+        0 trains at a fixed coefficient, an RD-sweep option the reference does not have)."""
         torch = _torch()
         rng = np.random.default_rng(self.seed)
         log = []
@@ -428,7 +430,7 @@ class Training:
                 step += 1
                 if x_val_path is not None and step % 10 == 0:
                     self._validate(x_val_path)
-            entropy_loss_coef += 0.01
+            entropy_loss_coef += coef_step
         return log
 
     def _validate(self, x_val_path: str) -> None:

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=0, help="stop each run after this many steps (0: all epochs)")
     ap.add_argument("--coefs", default="0.01,0.02,0.03")
+    ap.add_argument("--coef-step", type=float, default=0.01,
+                    help="coefficient increment per epoch (training.py:165: 0.01; 0 = fixed coefficient)")
     ap.add_argument("--seeds", default="0", help="weight-init / shuffling seeds per coefficient (label suffix _sN for N > 0)")
     ap.add_argument("--png-mode", default="tf", choices=("tf", "pillow"),
                     help="the PNG encoder of the entropy net's target (get_bpp: tf.image.encode_png settings)")
@@ -69,14 +71,14 @@ def main():
                 epochs = min(epochs, -(-args.steps * args.batch // args.epoch_samples))
             t1 = time.perf_counter()
             log = tr(x, None, max_epochs=epochs, batch_size=args.batch, entropy_loss_coef=coef, verbose=True,
-                     epoch_samples=args.epoch_samples)
+                     epoch_samples=args.epoch_samples, coef_step=args.coef_step)
             t_train = time.perf_counter() - t1
             if args.steps:
                 log = log[:args.steps]
             tr._save()
             w = W.load(os.path.join(d, "encoder"), "encoder")
             w.update(W.load(os.path.join(d, "decoder"), "decoder"))
-        label = f"coef{coef:.2f}" + (f"_s{seed}" if seed else "")
+        label = f"coef{coef:.2f}" + ("" if args.coef_step == 0.01 else f"_step{args.coef_step:g}") + (f"_s{seed}" if seed else "")
         sets[label] = w
         if args.save_dir:
             os.makedirs(args.save_dir, exist_ok=True)
@@ -90,7 +92,8 @@ def main():
                                             for k in ("ssim", "bpp")}}
         print(label, json.dumps(train_log[label]), flush=True)
     res = rd_sweep(sets, ev, tile=256)
-    out = {"config": f"config4: trained from entropy_loss_coef {args.coefs} (+0.01 per epoch, training.py:165), "
+    sched = "+0.01 per epoch, training.py:165" if args.coef_step == 0.01 else f"+{args.coef_step:g} per epoch, not the reference's +0.01"
+    out = {"config": f"config4: trained from entropy_loss_coef {args.coefs} ({sched}), "
                      f"{args.epochs} epochs of {args.epoch_samples} images, batch {args.batch}, on the reference's "
                      f"ImageNet patches ({len(x)} of them); evaluated on kodim21 768x512, whole and 256^2 tiles",
            "train": train_log, "points": {}}
