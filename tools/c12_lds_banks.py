@@ -1,0 +1,165 @@
+"""LDS bank model of conv12_kernel (nic_kernels.hip c12_wave): the LDS-array cycles per 8 x 8
+output tile of every LDS access the kernel makes, from the same address formulas, under the
+gfx950 banking rules of MI355X_MICROARCH.md section LDS (ds_read_b128: 4 x 16-lane groups, bank
+(a/4) mod 64; ds_read_b32: 2 x 32 lanes, bank (a/4) mod 32; ds_write_b128: 8 x 8 contiguous
+lanes, bank (a/4) mod 32; cycles per group = the most distinct dwords on one bank).
+
+    python tools/c12_lds_banks.py [--search]
+
+Per tile the model gives 970 extra (conflict) cycles; x 12,288 tiles (config 2) = 11,919,360,
+exactly SQ_LDS_BANK_CONFLICT of the round-5 PMC pass (profiles/r5z_traffic.json, conv2), and
+5,098 LDS cycles in all against 5,130 by SQ_LDS_IDX_ACTIVE (the patch LDS-DMA and flag words
+are not modelled).  --search runs the layout searches quoted in DESIGN.md section 5c.
+"""
+import argparse
+import random
+from collections import Counter
+
+HH = HW = 19            # conv2 halo (GeomS2<32, 8, 8>)
+HE = 10                 # odd columns start at record 10 (GeomS2::col)
+PSS, RPS = 10, 192      # record / row pitch in 16-B slots (PSB 160 B, RPB 3,072 B)
+PPW = 21                # patch row pitch, dwords (C12_PPW)
+NPT = (HH * HW + 15) // 16
+G128 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+        list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+G128 += [[l + 32 for l in g] for g in G128]
+G32 = [list(range(32)), list(range(32, 64))]
+G8 = [list(range(i, i + 8)) for i in range(0, 64, 8)]
+
+
+def cycles(addrs, width, groups, mod):
+    t = 0
+    for grp in groups:
+        banks = {}
+        for l in grp:
+            a = addrs[l]
+            if a is None:
+                continue
+            for d in range(width // 4):
+                dw = a // 4 + d
+                banks.setdefault(dw % mod, set()).add(dw)
+        t += max((len(s) for s in banks.values()), default=1)
+    return t
+
+
+def col(hx, he=HE):
+    return (hx & 1) * he + (hx >> 1)
+
+
+def stream_reads(pss=PSS, rps=RPS, he=HE):
+    """conv2 B fragments: per tile 25 taps x 4 pixel tiles x (hi, lo), one ds_read_b128 per
+    channel-group wave (x 4 waves), lane (g, l16) -> output pixel (2m + l16 / 8, l16 % 8)."""
+    c = 0
+    for kh in range(5):
+        for kw in range(5):
+            for m in range(4):
+                for hl in range(2):
+                    addrs = [(2 * (2 * m + ((l & 15) >> 3)) + kh) * rps * 16 + col(2 * ((l & 15) & 7) + kw, he) * pss * 16
+                             + (l >> 4) * 16 + hl * 64 for l in range(64)]
+                    c += cycles(addrs, 16, G128, 64)
+    return 4 * c, 4 * 25 * 4 * 2 * 4
+
+
+def patch_reads(ppw=PPW, slot=None, order=None, pad_partner=False):
+    """conv1 im2col from the split colour patch: per pixel tile 4 ds_read_b32 per plane (hi, lo);
+    lane (g, l16): pixel 16 pt + l16, tap pair slot[4 g + j] (kh = pr / 3, kw pair pr % 3).
+    The pad pair reads offset 0 (the kernel's poff) or, pad_partner, the partner group's element."""
+    slot = slot or list(range(16))
+    order = order or [(q // HW, q % HW) for q in range(HH * HW)]
+    c = 0
+    for pt in range(NPT):
+        for j in range(4):
+            addrs = []
+            for lane in range(64):
+                g, l16 = lane >> 4, lane & 15
+                q = 16 * pt + l16
+                hy, hx = order[q] if q < HH * HW else order[0]
+                pr = slot[4 * g + j]
+                if pr >= 15:  # pad pair (zero weight): any finite element
+                    pr = slot[4 * (g ^ 1) + j] if pad_partner else 0
+                addrs.append((2 * hy * ppw + hx + (pr // 3) * ppw + pr % 3) * 4)
+            c += 2 * cycles(addrs, 4, G32, 32)
+    return c, NPT * 4 * 2 * 2
+
+
+def halo_writes(pss=PSS, rps=RPS, he=HE):
+    """conv1 outputs into the conv2 halo: per pixel tile and 16-channel tile one ds_write_b128
+    (swap16_pair: even g the hi, odd g the lo of 8 channels)."""
+    c = 0
+    for pt in range(NPT):
+        for ct in range(2):
+            addrs = []
+            for lane in range(64):
+                g, l16 = lane >> 4, lane & 15
+                q = 16 * pt + l16
+                if q >= HH * HW:
+                    addrs.append(None)
+                    continue
+                hy, hx = q // HW, q % HW
+                addrs.append(hy * rps * 16 + col(hx, he) * pss * 16 + (g & 1) * 64 + (16 * ct + 4 * (g & ~1)) * 2)
+            c += cycles(addrs, 16, G8, 32)
+    return c, NPT * 2 * 8
+
+
+def partials():
+    """ts 1 partial sums: 4 waves x 4 ds_write_b128 + 4 waves x 4 ds_read_b128, lane-contiguous."""
+    return 4 * 4 * 8 + 4 * 4 * 4
+
+
+def search(seed=1):
+    # (1) affine halo layouts: record pitch, odd-column start, row pitch (LDS budget kept)
+    best = []
+    for pss in (8, 9, 10, 11, 12):
+        for he in (10, 11, 12):
+            for rps in range((19 if he == 10 else he + 9) * pss, 216):
+                if (19 * rps + 63) // 64 * 1024 * 2 + 16384 + 14336 + 16 > 163840:
+                    continue
+                r, ri = stream_reads(pss, rps, he)
+                w, wi = halo_writes(pss, rps, he)
+                best.append((r - ri + w - wi, r - ri, w - wi, pss, he, rps))
+    best.sort()
+    print("affine halo layouts, best (extra, reads, writes, pss, he, rps):", best[:3])
+    # (2) conv1 K-slot order x patch pitch, hill-climbed (pixel order: halo columns even-first)
+    order = []
+    for hy in range(19):
+        order += [(hy, x) for x in list(range(0, 19, 2)) + list(range(1, 19, 2))]
+    rnd = random.Random(seed)
+    top = (10 ** 9,)
+    for _ in range(20):
+        ppw = rnd.randrange(21, 33)
+        s = list(range(16))
+        rnd.shuffle(s)
+        e = patch_reads(ppw, s, order, True)[0]
+        improved = True
+        while improved:
+            improved = False
+            for i in range(16):
+                for k in range(i + 1, 16):
+                    s[i], s[k] = s[k], s[i]
+                    e2 = patch_reads(ppw, s, order, True)[0]
+                    if e2 < e:
+                        e, improved = e2, True
+                    else:
+                        s[i], s[k] = s[k], s[i]
+        if e < top[0]:
+            top = (e, ppw, s[:])
+    print("patch reads, best (cycles, pitch, slots):", top, "ideal", patch_reads()[1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--search", action="store_true")
+    args = ap.parse_args()
+    rows = [("conv2 stream ds_read_b128", stream_reads()), ("conv1 patch ds_read_b32", patch_reads()),
+            ("conv1 halo ds_write_b128", halo_writes()), ("partials b128", (partials(), partials()))]
+    tot = sum(c for _, (c, _) in rows)
+    extra = sum(c - i for _, (c, i) in rows)
+    for name, (c, i) in rows:
+        print(f"{name:28s} {c:6d} cycles/tile (conflict-free {i})")
+    print(f"total {tot} cycles/tile, conflict {extra} ({extra / tot:.3f}); x 12,288 tiles: {extra * 12288:,}")
+    if args.search:
+        search()
+
+
+if __name__ == "__main__":
+    main()
