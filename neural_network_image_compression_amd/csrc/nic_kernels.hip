@@ -1825,6 +1825,9 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   auto issue = [&](int i) {  // called for i = 0, 1, 2, ... in order
     int p, t0y, t0x;
     tile_take(w_issue, p, t0y, t0x);
+#ifdef NIC_DIAG_C8NODMA  // diagnostic build only: conv8 fetches the first two halos only (wrong results)
+    if (OUT_MODE == OUT_U8_LATENT && i > 1) return;
+#endif
     const int gy0 = 2 * t0y - a.pad_y, gx0 = 2 * t0x - a.pad_x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)a.in_s + (size_t)p * plane_bytes), (short)0, (int)plane_bytes, kBufWord3);
