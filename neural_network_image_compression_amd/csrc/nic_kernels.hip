@@ -2858,16 +2858,25 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
   TileWalk it_ld, it_run;
   it_ld.init(bi, nb, a.tiles_y, a.tiles_x);
   it_run = it_ld;
-  auto load_codes = [&](uint32_t (&cq)[D1A_LD]) __attribute__((always_inline)) {
+  // Buffer loads with an out-of-range offset (0) for pad pixels, issued unconditionally (a tile
+  // past the walk: an empty resource): with no branch around them the compiler counts them
+  // exactly and waits for a tile's codes with vmcnt(N), past the stores issued since, instead of
+  // vmcnt(0) (which exposed every tile's store latency: dconv1 0.056 -> 0.043 ms with the stores
+  // dropped, diagnostic build NIC_DIAG_D1NOST)
+  const size_t img_bytes = (size_t)a.H * a.W * 96;
+  auto load_codes = [&](uint32_t (&cq)[D1A_LD], bool live) __attribute__((always_inline)) {
     int pl, ty, tx;
     it_ld.take(pl, ty, tx);
-    const int p = p0 + pl;
-    const uint8_t* base = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
+    const int p = p0 + pl, type = p / a.nimg;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.in_u8 + (live ? (size_t)(p % a.nimg) * img_bytes + type * 32 : 0)), (short)0,
+        live ? (int)(img_bytes - type * 32) : 0, kBufWord3);
 #pragma unroll
     for (int j = 0; j < D1A_LD; ++j) {
       const int gy = ty * 8 - 1 + st_hy[j], gx = tx * 8 - 1 + st_hx[j];
       const bool ok = (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-      cq[j] = ok ? *(const uint32_t*)(base + ((size_t)gy * a.W + gx) * 96 + (threadIdx.x & 7) * 4) : 0u;
+      cq[j] = __builtin_amdgcn_raw_buffer_load_b32(
+          rs, ok ? (unsigned)(((gy * a.W + gx) * 96) + (threadIdx.x & 7) * 4) : kDmaOOR, 0, 0);
     }
   };
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);
@@ -2893,17 +2902,24 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     f32x4 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    f16x8 fb[MT];
+#ifndef NIC_D1_LA
+#define NIC_D1_LA 1  // B-fragment read-ahead in taps (A/B build: 2)
+#endif
+    f16x8 fb[NIC_D1_LA][MT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) fb[m] = frag(m, 0);
+    for (int u = 0; u < NIC_D1_LA; ++u)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        if (u < NTAPS) fb[u][m] = frag(m, u);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int t = 0; t < NTAPS; ++t) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t + 1], fb[m], acc[m], 0, 0, 0);  // w_lo*c
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t], fb[m], acc[m], 0, 0, 0);      // w_hi*c
-        if (t + 1 < NTAPS) fb[m] = frag(m, t + 1);
+        f16x8& cur = fb[t % NIC_D1_LA][m];
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t + 1], cur, acc[m], 0, 0, 0);  // w_lo*c
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[2 * t], cur, acc[m], 0, 0, 0);      // w_hi*c
+        if (t + NIC_D1_LA < NTAPS) cur = frag(m, t + NIC_D1_LA);
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
       }
     }
@@ -2921,7 +2937,16 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
       if (in) range_track(rmax, v);
       f16x4 hi, lo;
       split4(v, hi, lo);
+#ifdef NIC_DIAG_D1NOST  // diagnostic build only: every store dropped (out of range; wrong results)
+      __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), out_rs, kDmaOOR, 0, 0);
+#elif defined(NIC_DIAG_D1LIN)  // diagnostic build only: the same bytes as 1-KB contiguous stores (wrong layout)
+      {
+        const unsigned tq = (unsigned)(((ty0 >> 3) * a.tiles_x + (tx0 >> 3)) * 4 + py * 2 + px) * 4 + cg;
+        __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), out_rs, tq * 4096u + (unsigned)(m * 64 + lane) * 16u, 0, 0);
+      }
+#else
       __builtin_amdgcn_raw_buffer_store_b128(swap16_pair(hi, lo), out_rs, in ? out_org + g_off[m] : kDmaOOR, 0, 0);
+#endif
     }
   };
   auto step = [&](int i, uint32_t (&cq)[D1A_LD]) __attribute__((always_inline)) {
@@ -2939,20 +2964,31 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
     int pl, ty, tx;
     it_run.take(pl, ty, tx);
     if constexpr (NIC_D1A_PF == 2) {
-      if (i + 2 < ntile) load_codes(cq);  // tile i+2: lands during this tile's and the next's MFMAs
+      load_codes(cq, i + 2 < ntile);  // tile i+2: lands during this tile's and the next's MFMAs
     } else {  // A/B build: one tile ahead
-      if (i + 1 < ntile) load_codes(cq);
+      load_codes(cq, i + 1 < ntile);
     }
     phase(buf, &w1[0][0], std::integral_constant<int, KH1 * 4 + KW1>{}, PY1, PX1, p0 + pl, ty * 8, tx * 8);
     phase(buf, &w2[0][0], std::integral_constant<int, KH2 * 4 + KW2>{}, PY2, PX2, p0 + pl, ty * 8, tx * 8);
   };
-  load_codes(cqa);
+  load_codes(cqa, true);
   if constexpr (NIC_D1A_PF == 2) {
-    if (ntile > 1) load_codes(cqb);
-    for (int i = 0; i < ntile; i += 2) {
-      step(i, cqa);
-      if (i + 1 < ntile) step(i + 1, cqb);
+    load_codes(cqb, ntile > 1);
+    // 16 dropped stores (empty resource): the loop header then sees as many memory operations
+    // younger than cqa / cqb on entry as on the back edge (a tile's 8 stores, the next codes, the
+    // next tile's 8 stores), so the compiler's merged counter waits stay at vmcnt(18) instead of
+    // the prologue's vmcnt(2), which drained the last tile's stores before every other tile
+    {
+      const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_s, (short)0, 0, kBufWord3);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, none, kDmaOOR + 256u * k, 0, 0);
     }
+    int i = 0;
+    for (; i + 1 < ntile; i += 2) {  // no branch inside: the back edge's counter state is exact
+      step(i, cqa);
+      step(i + 1, cqb);
+    }
+    if (i < ntile) step(i, cqa);
   } else {
     for (int i = 0; i < ntile; ++i) step(i, cqa);
   }
