@@ -4,7 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out
-# the 19,000 patches travel as one tar (a directory of them overflows the upload's entry limit)
+# the 19,000 patches travel as one tar (a directory of them overflows the upload's entry limit;
+# .gpurunignore lists the tar: drop that line for a training call)
 if [ ! -d data/imagenet_patches_full ] && [ -f data/imagenet_patches_full.tar ]; then
   tar xf data/imagenet_patches_full.tar -C data || exit 1
 fi
