@@ -2861,8 +2861,9 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
   // Buffer loads with an out-of-range offset (0) for pad pixels, issued unconditionally (a tile
   // past the walk: an empty resource): with no branch around them the compiler counts them
   // exactly and waits for a tile's codes with vmcnt(N), past the stores issued since, instead of
-  // vmcnt(0) (which exposed every tile's store latency: dconv1 0.056 -> 0.043 ms with the stores
-  // dropped, diagnostic build NIC_DIAG_D1NOST)
+  // vmcnt(0), which drained the previous tile's stores first (0.0555 vs 0.0568-0.0572 ms,
+  // profiles/r5n_d1_ab; the stores themselves cost ~13 us: 0.043 ms with them dropped,
+  // diagnostic build NIC_DIAG_D1NOST)
   const size_t img_bytes = (size_t)a.H * a.W * 96;
   auto load_codes = [&](uint32_t (&cq)[D1A_LD], bool live) __attribute__((always_inline)) {
     int pl, ty, tx;
