@@ -1114,6 +1114,36 @@ struct HaloPieces {
 // left or right image edge, retargets the slots of out-of-image columns out of range.
 constexpr unsigned kDmaOOR = 0x80000000u;  // an offset past any plane: the DMA writes zeros
 constexpr int kBufWord3 = 0x00020000;      // gfx9 raw-buffer resource word 3
+#ifdef NIC_DIAG_KTIME  // diagnostic build only: first-wave start / last-wave exit of each kernel (100 MHz clock)
+__device__ unsigned long long g_ktime[16][2];
+#define KT_BEGIN(sl)                                                                         \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0) atomicMin(&g_ktime[sl][0], __builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+#define KT_END(sl)                                                                           \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0) atomicMax(&g_ktime[sl][1], __builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+struct KtGuard {
+  int sl;
+  __device__ explicit KtGuard(int s) : sl(s) { KT_BEGIN(s); }
+  __device__ ~KtGuard() { KT_END(sl); }
+};
+#define KT_SCOPE(sl) KtGuard kt_guard_(sl)
+extern "C" int nic_diag_ktime(unsigned long long* out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ktime), sizeof(g_ktime)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long init[16][2];
+    for (int k = 0; k < 16; ++k) init[k][0] = ~0ull, init[k][1] = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ktime), init, sizeof(init)) != hipSuccess) return -1;
+  }
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#else
+#define KT_BEGIN(sl) do { } while (0)
+#define KT_END(sl) do { } while (0)
+#define KT_SCOPE(sl) do { } while (0)
+#endif
 
 __device__ __forceinline__ void dma16_buf(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, char* lds_wave_base) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)lds_wave_base, 16, (int)voff, 0, 0, 0);
@@ -2191,6 +2221,7 @@ void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int*
 // Grid (ceil(hp * wp / 2 / 256), N): the image is blockIdx.y, the rest 32-bit index math.
 __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __restrict__ rgb, uint16_t* __restrict__ cp,
                                                            int N, int H, int W, int oy, int ox, int hp, int wp) {
+  KT_SCOPE(0);
   const int pairs = wp / 2;
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= hp * pairs) return;
@@ -2541,6 +2572,7 @@ __device__ __forceinline__ int xcd_pos(int b, int nb) {
 }
 
 __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
+  KT_SCOPE(1);
   using G = GeomS2<32, 8, 8>;
   __shared__ __attribute__((aligned(16)))
   char lds[2 * G::HALO_BYTES + 4 * 4 * 1024 + 4 * C12_PLANE + 16];
@@ -2556,6 +2588,7 @@ __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
 
 template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1, bool HIST = false>
 __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
+  KT_SCOPE(3);
   using G = GeomS2<CIN, TH, 8>;
   constexpr int NCG = COUT / 16;
   static_assert(NCG * NTS == 8, "8 waves per block");
@@ -2578,6 +2611,7 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
 // (the phase of a transposed layer).
 template <int CIN, int COUT, int TH, int TW, bool RESID, bool TRP, bool PROJ = false>
 __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a) {
+  KT_SCOPE(6);
   using G = GeomWS<CIN, TH, TW>;
   __shared__ __attribute__((aligned(16)))
   char lds[2 * G::HALO_BYTES + (PROJ ? 2 * (CIN / 32) * 2 * 64 * 16 + TH * TW * COUT * 4 : 0) +
@@ -2997,6 +3031,7 @@ __device__ __forceinline__ void d1all_wave(const ConvArgs& a, char* lds, int mod
 }
 
 __global__ __launch_bounds__(512, 1) void dconv1_all_kernel(ConvArgs a) {
+  KT_SCOPE(5);
   __shared__ __attribute__((aligned(16))) char lds[2 * D1_HB];
   const int gi = (int)blockIdx.x >= a.ws_blk[1] ? 1 : 0;
   const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
@@ -3058,6 +3093,7 @@ struct K3Ranges {
 };
 template <int MT, bool SKEW, bool STRIP>
 __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a, K3Ranges rng) {
+  KT_SCOPE(2);
   constexpr int COUT = 64, KST = 2;
   __shared__ __attribute__((aligned(16))) char lds[K3P_LDS];
   char* in_ring = lds;
@@ -3669,6 +3705,7 @@ __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
 // projection planes.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
+  KT_SCOPE(7);
   // XCD-aware order: blocks are dealt round-robin to the 8 XCDs, so block L runs on XCD
   // L % 8; give each XCD a contiguous raster range of (image, tile) instead, so neighbouring
   // tiles -- which read each other's edge projections -- share that XCD's L2
@@ -4529,6 +4566,7 @@ __device__ __forceinline__ bool grid_barrier(int* bar, int nb, unsigned long lon
 }
 
 __global__ __launch_bounds__(256, 2) void fp32_chain_kernel(Fp32Chain ch) {
+  KT_SCOPE(4);
   __shared__ __attribute__((aligned(16))) float lds[kChainLds];
   if (range_gated_off(ch.gate)) return;  // whole grid: the gate word is the same for every block
   if (chain_timed_out(ch.bar)) return;   // an earlier chain on this ctx timed out (not yet reported)
