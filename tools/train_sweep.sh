@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: config-4 training sweeps on the full patch set (needs data/imagenet_patches_full in
+# config-4 training sweeps on the full patch set (needs data/imagenet_patches_full in
 # the upload, or data/imagenet_patches_full.tar): COEFS, SEEDS, STEP (coefficient increment per epoch), TAG
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
