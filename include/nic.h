@@ -94,18 +94,15 @@ enum { NIC_PRECISION_FP32 = 0, NIC_PRECISION_F16X3 = 1 };
  *   NIC_RANGE_ERROR -- the call synchronises its stream after the split pass and returns
  *     NIC_ERANGE if it tripped (outputs undefined).
  * nic_range_trips (synchronising) counts the passes that tripped since nic_create.
- * A FALLBACK re-run runs as one chained launch with a bounded grid barrier; should that barrier
- * ever time out (blocks not co-resident), the ctx marks it and every later chained re-run on the
- * ctx exits at entry -- so device-pointer FALLBACK calls of that window that trip return NIC_OK
- * with the split pass's (undefined) outputs -- until the next synchronising call
- * (nic_range_trips, an ERROR-policy call or a host-array call) reports NIC_EHIP once and
- * clears the mark. */
+ * A FALLBACK re-run runs as one chained launch whose stages hand their tiles out through
+ * device-side queues (no grid barrier): it completes whatever share of the grid is resident,
+ * so a tripped FALLBACK call always returns the exact-fp32 outputs. */
 enum { NIC_RANGE_FALLBACK = 0, NIC_RANGE_ERROR = 1 };
 int nic_set_range_policy(nic_ctx* ctx, int policy);
 int nic_range_trips(nic_ctx* ctx, int64_t* passes);
 /* How the chained exact-fp32 re-run launches on ctx's device: its resident blocks per CU
- * (occupancy; the grid is one block per CU and its grid barrier needs them all resident),
- * the grid, and whether it uses a cooperative launch (1) or a plain one (0). */
+ * (occupancy; informational -- the queued stages need no co-residency), the grid (one block
+ * per CU) and whether it uses a cooperative launch (always 0: a plain launch). */
 int nic_rerun_launch_info(nic_ctx* ctx, int* blocks_per_cu, int* grid, int* cooperative);
 
 /* ABI version: major * 10000 + minor * 100 + patch */
@@ -181,7 +178,9 @@ int nic_entropy_hist(nic_ctx* ctx, const uint8_t* latent, int n, int h8, int w8,
 int nic_encode_entropy(nic_ctx* ctx, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
                        float* bits, void* stream);
 /* 1 in *folds when nic_encode_entropy on (n, h, w) images (counts or bits requested) takes the
- * folded form on ctx's device and precision, 0 when it runs the two calls. */
+ * folded form on ctx's device and precision, 0 when it runs the two calls.  Shapes the call
+ * refuses (NIC_ESHAPE: bad sizes, n > 21845, latent planes over 2^31 / 6 codes) and n = 0 are
+ * refused the same way. */
 int nic_encode_entropy_fold(nic_ctx* ctx, int n, int h, int w, int* folds);
 
 /* MS-SSIM of tf.image.ssim_multiscale(a, b, max_val=255) (tf2_0/tests/calc_ssim.py:13)

@@ -180,6 +180,10 @@ def _host_threads() -> int:
         return max(1, os.cpu_count() or 1)
 
 
+WRITES_IN_FLIGHT = 2  # batches handed to the PNG writer and not yet written (use_model)
+BATCH_PIXELS = 64 * 512 * 768  # pixels staged per device batch (use_model): 64 Kodak-sized images, 3 4K frames
+
+
 def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, in_cshape: int,
               batch_size: int = 64, workers=None) -> None:
     """utils.py:46-62: every colour image of ``dataset_path`` (sorted; read_dataset's filter)
@@ -188,9 +192,11 @@ def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, i
     ``workers=0`` is the reference's serial loop (read everything, then batches of
     ``batch_size`` -- the reference's 4 -- each run and saved inline).  Otherwise (default) a
     pipeline over the host cores: images are decoded by a reader pool in file order, consecutive
-    equal-shaped images are fed to the device ``batch_size`` (64) at a time, and each batch's PNG
-    files are encoded natively on ``workers`` threads (default: every CPU this process may use,
-    at most 16) while the next batches are read and run.  Every image's output depends on that
+    equal-shaped images are fed to the device ``batch_size`` (64) at a time (at most
+    ``BATCH_PIXELS`` pixels), and each batch's PNG files are encoded natively on ``workers``
+    threads (default: every CPU this process may use, at most 16) while the next batches are
+    read and run; at most ``WRITES_IN_FLIGHT`` batches wait for the writer, so host memory stays
+    bounded however large the directory.  Every image's output depends on that
     image alone (the kernels are batch-invariant), so the files are byte-identical either way."""
     os.makedirs(output_dir, exist_ok=True)
     model.load(checkpoint_path)
@@ -209,15 +215,17 @@ def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, i
         pending = [readers.submit(_read_one, os.path.join(dataset_path, fn)) for fn in files[:depth]]
 
         def flush():
-            nonlocal futures
             if batch:
-                futures += feed_batch(model, np.stack(batch), list(names), output_dir, in_cshape, pool=writer,
-                                      png_threads=png_threads)
+                # bounded host memory: at most WRITES_IN_FLIGHT batches' outputs wait for the
+                # (slower) PNG writer; the device pass of the next batch still overlaps them
+                while len(futures) >= WRITES_IN_FLIGHT:
+                    futures.pop(0).result()  # re-raises a write error
+                futures.extend(feed_batch(model, np.stack(batch), list(names), output_dir, in_cshape, pool=writer,
+                                          png_threads=png_threads))
                 batch.clear()
                 names.clear()
-            for f in [f for f in futures if f.done()]:
-                f.result()  # re-raise a write error early
-            futures = [f for f in futures if not f.done()]
+            while futures and futures[0].done():
+                futures.pop(0).result()  # re-raise a write error early
 
         for k, fn in enumerate(files):
             a = pending[k].result()
@@ -226,7 +234,8 @@ def use_model(model, dataset_path: str, checkpoint_path: str, output_dir: str, i
             pending[k] = None
             if a.ndim != 3:  # read_dataset keeps colour (3-D) images only
                 continue
-            if batch and (a.shape != batch[0].shape or len(batch) >= batch_size):
+            if batch and (a.shape != batch[0].shape or len(batch) >= batch_size
+                          or (len(batch) + 1) * a.shape[0] * a.shape[1] > BATCH_PIXELS):
                 flush()
             batch.append(a.astype(np.uint8, copy=False))
             names.append(".".join(fn.split(".")[:-1]))

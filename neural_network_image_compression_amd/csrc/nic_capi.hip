@@ -514,7 +514,9 @@ int nic_create(int device, nic_ctx** out) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: weight allocation failed");
   }
-  if (hipMalloc(&c->range, 8 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(int)) != hipSuccess ||
+  // range words: [0] split pass epoch that tripped, [1] re-runs, [2..] the chained re-run's queue
+  static_assert(2 + kChainQWords <= 32, "range words");
+  if (hipMalloc(&c->range, 32 * sizeof(int)) != hipSuccess || hipMemset(c->range, 0, 32 * sizeof(int)) != hipSuccess ||
       hipHostMalloc(&c->range_host, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     nic_destroy(c);
     return fail(NIC_ENOMEM, "nic_create: range-guard allocation failed");
@@ -719,7 +721,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   Fp32Chain chain{};
   const bool chained = !x3 && rg.gate && use_chain();
   chain.gate = rg;
-  chain.bar = c->range + 2;
+  chain.q = c->range + 2;
   // f16x3: conv1 runs inside the conv2 kernel (launch_conv12_x3, timed as conv2)
   const bool fuse12 = x3 && conv12_fused();
   if (!fuse12) TIMED(L_CONV1, chained ? chain_add_conv1(chain, a1) : launch_conv1(a1, st));
@@ -813,7 +815,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   Fp32Chain chain{};  // the gated exact-fp32 re-run as one launch (see encode_pass)
   const bool chained = !x3 && rg.gate && use_chain();
   chain.gate = rg;
-  chain.bar = c->range + 2;
+  chain.q = c->range + 2;
   auto run = [&](LayerId id, const ConvArgs& a) {
     return chained ? chain_add_layer(chain, id, a) : x3 ? launch_layer_x3(id, a, st) : launch_layer(id, a, st);
   };
@@ -902,17 +904,6 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
 // run the exact-fp32 kernels (64-bit addressing) instead of failing (nic.h).
 bool x3_plane_fits(long long h64, long long w64) { return h64 * w64 * 64 * 4 < (1LL << 30); }
 
-// The chained re-run's barrier timeout (nic_kernels.hip grid_barrier), read from words[4] of
-// c->range with the device idle: reported once as NIC_EHIP, and the barrier words (arrivals,
-// generation, flag) are zeroed so the next chain starts clean (an abandoned barrier leaves
-// bar[0] mid-count; until this clears the sticky flag, every chain on the ctx exits at entry).
-int chain_timeout_check(nic_ctx* c, const int* words, const char* what) {
-  if (!words[4]) return NIC_OK;
-  HIP_TRY(hipMemset(c->range + 2, 0, 3 * sizeof(int)));
-  return fail(NIC_EHIP, "%s: a chained exact-fp32 re-run timed out at its grid barrier (blocks not co-resident); "
-              "the outputs of that pass are undefined", what);
-}
-
 template <class Pass>
 int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pass) {
   if (c->precision != NIC_PRECISION_F16X3 || !x3_fits) return pass(false, RangeGuard{}, true);
@@ -929,13 +920,8 @@ int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pas
     gate.epoch = c->epoch;
     return pass(false, gate, false);
   }
-  HIP_TRY(hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(c->range_host, c->range, sizeof(int), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (c->range_host[4]) {  // an earlier FALLBACK pass's chain timed out
-    HIP_TRY(hipDeviceSynchronize());
-    rc = chain_timeout_check(c, c->range_host, what);
-    if (rc) return rc;
-  }
   if (*c->range_host == c->epoch) {
     ++c->error_trips;
     return fail(NIC_ERANGE, "%s: an activation reached the f16 limit of the split-f16 pass (|x| >= 65504); "
@@ -1157,13 +1143,6 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     }
     ++issued;
   }
-  // the range-guard words behind the last pass (its chained re-run's barrier timeout flag),
-  // read once the streams drain: this call synchronises anyway
-  const bool chain_check = !err && issued > 0 && c->precision == NIC_PRECISION_F16X3 &&
-                           c->range_policy == NIC_RANGE_FALLBACK;
-  if (chain_check && (hipMemcpyAsync(c->range_host, c->range, 5 * sizeof(int), hipMemcpyDeviceToHost, c->hs[1]) != hipSuccess ||
-                      hipEventRecord(c->hev_caller, c->hs[1]) != hipSuccess))
-    err = fail(NIC_EHIP, "host surface: range-word read-back failed");
   for (int k = 0; k < issued && !err; ++k) {  // chunk k's unstaging overlaps chunk k+1's work
     hipError_t e = host_wait(c->hev[2][k]);
     if (e != hipSuccess) {
@@ -1173,18 +1152,10 @@ int host_pipeline(nic_ctx* c, const uint8_t* in, size_t in_row, uint8_t* out, si
     if (!out_pin) CopyPool::get().copy(out + lo[k] * out_row, c->pin_out + lo[k] * out_row, (lo[k + 1] - lo[k]) * out_row);
   }
   // success: every copy-in fed a pass and every pass a copy-out, so the last copy-out's event
-  // (and the read-back's) means all three streams are idle -- no stream synchronisations
-  // (~10-30 us per call); any error path drains them
-  if (!err && issued == K && chain_check) {
-    hipError_t e = host_wait(c->hev_caller);
-    if (e != hipSuccess) err = fail(NIC_EHIP, "host surface: %s", hipGetErrorString(e));
-  }
+  // means all three streams are idle -- no stream synchronisations (~10-30 us per call); any
+  // error path drains them
   if (err || issued != K)
     for (int i = 0; i < 3; ++i) (void)hipStreamSynchronize(c->hs[i]);
-  if (!err && chain_check && c->range_host[4]) {
-    HIP_TRY(hipDeviceSynchronize());
-    err = chain_timeout_check(c, c->range_host, "host surface");
-  }
   return err;
 }
 
@@ -1290,9 +1261,21 @@ static bool encode_entropy_folds(const nic_ctx* c, int n, int h, int w) {
          hist_fold_supported(n, eg.c8y.out, eg.c8x.out);
 }
 
+// the shape limits nic_encode_entropy applies (shared with the fold query, so the query never
+// reports a form for a shape the call refuses)
+static int encode_entropy_shape(const char* fn, int n, int h, int w) {
+  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "%s: bad input shape (%d,%d,%d,3)", fn, n, h, w);
+  if (3LL * n > 65535) return fail(NIC_ESHAPE, "%s: batch %d exceeds 21845 images per call", fn, n);
+  int h8, w8;
+  nic_latent_shape(h, w, &h8, &w8);
+  if ((long long)h8 * w8 * 6 > 0x7fffffffLL) return fail(NIC_ESHAPE, "%s: latent %dx%d too large", fn, h8, w8);
+  return NIC_OK;
+}
+
 int nic_encode_entropy_fold(nic_ctx* c, int n, int h, int w, int* folds) {
   if (!c || !folds) return fail(NIC_EINVAL, "nic_encode_entropy_fold: NULL argument");
-  if (n <= 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode_entropy_fold: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (n == 0) return fail(NIC_ESHAPE, "nic_encode_entropy_fold: empty batch");
+  if (int rc = encode_entropy_shape("nic_encode_entropy_fold", n, h, w)) return rc;
   DeviceGuard guard(c->device);
   *folds = encode_entropy_folds(c, n, h, w) ? 1 : 0;
   return NIC_OK;
@@ -1301,16 +1284,14 @@ int nic_encode_entropy_fold(nic_ctx* c, int n, int h, int w, int* folds) {
 int nic_encode_entropy(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* latent, uint32_t* counts,
                        float* bits, void* stream) {
   if (!c) return fail(NIC_EINVAL, "nic_encode_entropy: NULL ctx");
-  if (n < 0 || h <= 0 || w <= 0) return fail(NIC_ESHAPE, "nic_encode_entropy: bad input shape (%d,%d,%d,3)", n, h, w);
+  if (int rc = encode_entropy_shape("nic_encode_entropy", n, h, w)) return rc;
   if (!models_ready(c, 0)) return fail(NIC_ENOWEIGHTS, "nic_encode_entropy: encoder weights not fully set");
   if (n == 0) return NIC_OK;
   if (!rgb || !latent) return fail(NIC_EINVAL, "nic_encode_entropy: NULL buffer");
-  if (3LL * n > 65535) return fail(NIC_ESHAPE, "nic_encode_entropy: batch %d exceeds 21845 images per call", n);
   DeviceGuard guard(c->device);
   hipStream_t st = (hipStream_t)stream;
   const EncGeom eg = enc_geom(n, h, w);
   const int h8 = eg.c8y.out, w8 = eg.c8x.out;
-  if ((long long)h8 * w8 * 6 > 0x7fffffffLL) return fail(NIC_ESHAPE, "nic_encode_entropy: latent %dx%d too large", h8, w8);
   const bool fits = x3_plane_fits(eg.c2y.out, eg.c2x.out);
   // the fold needs the split-f16 pass with the tap-split conv8 and block ranges within a plane;
   // otherwise (and for counts == bits == NULL) the two-step form
@@ -1515,10 +1496,10 @@ int nic_range_trips(nic_ctx* c, int64_t* passes) {
   if (!c || !passes) return fail(NIC_EINVAL, "nic_range_trips: NULL argument");
   DeviceGuard guard(c->device);
   HIP_TRY(hipDeviceSynchronize());
-  int words[5] = {};
+  int words[2] = {};
   HIP_TRY(hipMemcpy(words, c->range, sizeof(words), hipMemcpyDeviceToHost));
   *passes = (int64_t)words[1] + c->error_trips;
-  return chain_timeout_check(c, words, "nic_range_trips");  // reported once, then cleared
+  return NIC_OK;
 }
 
 int nic_rerun_launch_info(nic_ctx* c, int* blocks_per_cu, int* grid, int* cooperative) {

@@ -116,15 +116,13 @@ struct Dconv8Args {
 // The gated exact-fp32 re-run of a split-f16 pass as one launch (stages run in
 // order with grid barriers; every block exits at once unless gate.gate == gate.epoch).
 constexpr int kChainMax = 6;
+constexpr int kChainQWords = 2 * kChainMax + 1;  // Fp32Chain::q
 struct Fp32Chain {
   RangeGuard gate;  // gate + trips of the re-run (the stages' own rg fields are unused)
-  int* bar;         // 3 zeroed device words: barrier arrivals, generation, timeout flag
+  int* q;           // kChainQWords zeroed device words: per stage next tile, tiles done; blocks out
   int nstage;
-  // bounded barrier wait (s_memrealtime ticks, 100 MHz; launch_fp32_chain fills it) and a
-  // diagnostic that keeps the grid's last block from ever arriving (NIC_DIAG_BARRIER=skip:
-  // the timeout path's GPU test, tests/barrier_timeout_check.py)
-  unsigned long long timeout_ticks;
-  int diag_skip;
+  int diag_late;    // NIC_DIAG_CHAIN (launch_fp32_chain fills it): block 0 starts ~1 ms late
+  int total[kChainMax];     // tiles of each stage
   int kind[kChainMax];      // LayerId; L_CONV1 -> c1, L_DCONV8 -> d8, other layers -> c[s]
   ConvArgs c[kChainMax];
   Conv1Args c1;

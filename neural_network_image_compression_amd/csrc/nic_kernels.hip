@@ -131,6 +131,17 @@ __device__ __forceinline__ bool range_gated_off(const RangeGuard& rg) {
   return false;
 }
 
+// The chained re-run's tile queue (fp32_chain_kernel): the block takes its next tile of a
+// stage with one block-uniform atomicAdd, so tiles go only to blocks that are running -- the
+// chain needs no co-resident grid (a block that starts late finds the stage's queue empty).
+__device__ __forceinline__ int chain_take(int* q) {
+  __shared__ int s_job;
+  __syncthreads();  // the previous tile's LDS use is done; s_job is free
+  if (threadIdx.x == 0) s_job = atomicAdd(q, 1);
+  __syncthreads();
+  return s_job;
+}
+
 // ((t0*k0 + t1*k1) + t2*k2), every op rounded (utils.py:64-68)
 __device__ __forceinline__ float project(const float* k, float t0, float t1, float t2) {
   return __fadd_rn(__fadd_rn(__fmul_rn(t0, k[0]), __fmul_rn(t1, k[1])), __fmul_rn(t2, k[2]));
@@ -242,15 +253,16 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, int p, int model, 
   }
 }
 
-// Body of one block (b0 of nb) over its (plane, tile) jobs, grid-stride; `lds` holds
-// G::LDS_FLOATS floats.  Called by conv_mfma_kernel and by the chained gated re-run
-// (fp32_chain_kernel).
+// Body of one block (b0 of nb) over its (plane, tile) jobs, grid-stride -- or, with a queue
+// q (the chained gated re-run, fp32_chain_kernel), the tiles it takes from q; `lds` holds
+// G::LDS_FLOATS floats.  Returns the number of tiles the block ran.
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
           int OUT_MODE, bool RESID>
-__device__ __forceinline__ void conv_mfma_body(const ConvArgs& a, float* lds, int b0, int nb) {
+__device__ __forceinline__ int conv_mfma_body(const ConvArgs& a, float* lds, int b0, int nb, int* q = nullptr) {
   using G = ConvGeom<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK>;
   const int per_plane = a.tiles_y * a.tiles_x;
-  for (int job = b0; job < per_plane * a.P; job += nb) {
+  int ran = 0;
+  for (int job = q ? chain_take(q) : b0; job < per_plane * a.P; job = q ? chain_take(q) : job + nb, ++ran) {
   __syncthreads();  // every wave is done with the previous job's LDS
   const int p = job / per_plane;
   const int tile = job - p * per_plane;
@@ -419,6 +431,7 @@ __device__ __forceinline__ void conv_mfma_body(const ConvArgs& a, float* lds, in
     }
   }
   }  // job
+  return ran;
 }
 
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
@@ -2220,8 +2233,12 @@ void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int*
 // One thread per (image, padded row, 4 columns): the three colour planes of four pixels, split
 // into hi / lo f16 (zero outside the image), one 8-B store per plane and half (the plane width
 // is a multiple of 4).  The 12 RGB bytes of 4 interior pixels are read as 4 aligned dwords of
-// the image row (a buffer resource: bytes past the row read 0) and re-aligned by v_alignbyte;
-// border quads read pixel by pixel.  Grid (ceil(hp * wp / 4 / 256), N): the image is blockIdx.y.
+// the image row (a buffer resource over the row) and re-aligned by v_alignbyte; border quads
+// read pixel by pixel.  A dword that straddles the row's end is not guaranteed to return its
+// in-range bytes, so a quad takes the dword path only when every dword it uses lies inside the
+// row (d[3] is used iff the byte shift is non-zero).  With conv1 / conv2's SAME offsets
+// (ox = 3, 4, 5, 6 for W = 0, 3, 2, 1 mod 4) the last interior quad never needs a straddling
+// dword, so the byte path only ever takes the true borders.  Grid (ceil(hp * wp / 4 / 256), N): the image is blockIdx.y.
 // (Two columns per thread with byte loads: 20.9 vs 20.1 us per launch, profiles/r5w_*.)
 __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __restrict__ rgb, uint16_t* __restrict__ cp,
                                                             int N, int H, int W, int oy, int ox, int hp, int wp) {
@@ -2240,10 +2257,10 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
 #pragma unroll
     for (int k = 0; k < 3; ++k) v[k][e] = __fadd_rn(project(c_ycbcr + 3 * k, r8, g8, b8), c_ycbcr_off[k]);
   };
-  if (row_in && x0 >= 0 && x0 + 3 < W) {
+  const unsigned b0 = 3u * (unsigned)x0, a0 = b0 & ~3u, sh = b0 & 3u;
+  if (row_in && x0 >= 0 && x0 + 3 < W && (sh == 0 || a0 + 16u <= 3u * (unsigned)W)) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(rgb + ((size_t)n * H + y) * W * 3), (short)0, W * 3, kBufWord3);
-    const unsigned b0 = 3u * (unsigned)x0, a0 = b0 & ~3u, sh = b0 & 3u;
     unsigned d[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, a0 + 4u * i, 0, 0);
@@ -2482,7 +2499,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the stream order
     });
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(NIC_C12_PRIO == 2 && TS == 0 ? 2 : 0);
   };
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
   // epilogue of tile i (called for i = 0, 1, 2, ... in order by the ts 0 waves): its own sums +
@@ -2522,6 +2539,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
   lds_reads_done();
   stage_barrier();  // patches 0, 1 complete
   if (ntile > 0) conv1(0);
+  if constexpr (NIC_C12_PRIO == 2 && TS == 0) __builtin_amdgcn_s_setprio(2);  // A/B: ts 0's whole chain first
 #ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
   unsigned long long sx[8] = {}, sa, sb;
   const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
@@ -3472,10 +3490,11 @@ constexpr int C1_HE = (C1_HH + 1) / 2;     // 18 even columns, then 17 odd ones
 constexpr int C1_PS = 40;
 
 constexpr int C1_LDS_FLOATS = C1_HH * C1_PS;
-__device__ __forceinline__ void conv1_colour_body(const Conv1Args& a, float* plane, int b0, int nb) {
+__device__ __forceinline__ int conv1_colour_body(const Conv1Args& a, float* plane, int b0, int nb, int* q = nullptr) {
   float rmax = 0.f;  // range guard of the split output
   const int per_plane = a.tiles_y * a.tiles_x;
-  for (int job = b0; job < per_plane * a.P; job += nb) {  // grid-stride, as conv_mfma
+  int ran = 0;  // grid-stride or queued, as conv_mfma_body
+  for (int job = q ? chain_take(q) : b0; job < per_plane * a.P; job = q ? chain_take(q) : job + nb, ++ran) {
   __syncthreads();  // the previous job's plane reads are done
   const int p = job / per_plane, tile = job - p * per_plane;
   const int n = p % a.nimg, type = p / a.nimg;
@@ -3572,6 +3591,7 @@ __device__ __forceinline__ void conv1_colour_body(const Conv1Args& a, float* pla
   }
   }  // job
   range_report(a.rg, rmax);
+  return ran;
 }
 
 __global__ __launch_bounds__(256) void conv1_colour_kernel(Conv1Args a) {
@@ -3651,9 +3671,10 @@ constexpr int D8_LDS_FLOATS = D8_HH * D8_HW * D8_PS;
 // UNR: channel-quad unroll (2 in the standalone kernel; 1 inside fp32_chain_kernel, whose
 // register budget is that of two resident blocks per CU)
 template <int UNR = 2>
-__device__ __forceinline__ void dconv8_colour_body(const Dconv8Args& a, float* halo, int b0, int nb) {
+__device__ __forceinline__ int dconv8_colour_body(const Dconv8Args& a, float* halo, int b0, int nb, int* q = nullptr) {
   const int per_img = a.tiles_y * a.tiles_x;
-  for (int job = b0; job < per_img * a.nimg; job += nb) {  // grid-stride, as conv_mfma
+  int ran = 0;  // grid-stride or queued, as conv_mfma_body
+  for (int job = q ? chain_take(q) : b0; job < per_img * a.nimg; job = q ? chain_take(q) : job + nb, ++ran) {
   const int n = job / per_img, tile = job - n * per_img;
   const int tyi = tile / a.tiles_x;
   const int t0y = tyi * D8_TH, t0x = (tile - tyi * a.tiles_x) * D8_TW;
@@ -3718,6 +3739,7 @@ __device__ __forceinline__ void dconv8_colour_body(const Dconv8Args& a, float* h
   const int my = t0y + ty, mx = t0x + tx;
   if (my < a.H && mx < a.W) d8_store_rgb(a, n, my, mx, outv);
   }  // job (the next job's first step barrier orders the halo reuse)
+  return ran;
 }
 
 __global__ __launch_bounds__(256) void dconv8_colour_kernel(Dconv8Args a) {
@@ -4536,11 +4558,18 @@ __global__ __launch_bounds__(256) void unpack_latent_kernel(const uint8_t* __res
 // smaller grid drains faster; a tripped pass re-runs on fewer, longer-lived blocks)
 // ------------------------------------------------------------------------------------
 // The gated exact-fp32 re-run of a split-f16 pass as ONE launch: every stage of the pass
-// (conv1 / conv_mfma layers / dconv8) in sequence, a grid barrier between stages.  When
-// the split pass stayed in range every block exits at the gate, so the pass costs one
-// dispatch instead of one per layer (each dispatch, even of an empty kernel, holds the
-// queue for ~5 us: measured 4.7-5.3 us for 1 to 256 blocks).  One block per CU (all
-// resident, as the barrier needs).
+// (conv1 / conv_mfma layers / dconv8) in sequence.  When the split pass stayed in range every
+// block exits at the gate, so the pass costs one dispatch instead of one per layer (each
+// dispatch, even of an empty kernel, holds the queue for ~5 us: measured 4.7-5.3 us for 1 to
+// 256 blocks).
+//
+// No grid barrier, so no co-residency requirement: the tiles of stage s are handed out by a
+// queue word (chain_take); a block that has run its share adds its tile count to the stage's
+// done word (release) and, before taking tiles of stage s+1, waits for done == the stage's
+// tile total (acquire).  Every tile taken is held by a running block that never waits while it
+// holds one, so the totals are always reached: blocks that start late (other streams' kernels
+// on the CUs, a grid larger than fits) find the queues drained and pass through.  The last
+// block to leave zeroes the words for the next chain on the ctx (stream-ordered).
 // ------------------------------------------------------------------------------------
 template <class... Gs>
 constexpr int max_lds_floats() {
@@ -4555,72 +4584,58 @@ using G_d1 = ConvGeom<32, 64, 5, 2, true, 8, 8, 2, 2, 1>;
 using G_d7 = ConvGeom<64, 64, 5, 2, true, 8, 16, 4, 1, 1>;
 constexpr int kChainLds = std::max({max_lds_floats<G_c2, G_k3, G_c8, G_d1, G_d7>(), C1_LDS_FLOATS, D8_LDS_FLOATS});
 
-// grid barrier over nb blocks: bar[0] arrivals (back to 0 after every barrier), bar[1]
-// generation.  Vector atomics and agent-scope fences (stage outputs visible across XCDs).
-// The wait is bounded: the launch guarantees co-residency (cooperative launch, grid <= CUs x
-// the occupancy checked on the host), but should a block never arrive the waiters give up
-// after `ticks` (~2 s of s_memrealtime, 100 MHz), set the sticky flag bar[2] and the kernel
-// exits instead of hanging the queue.  Returns false after a timeout.  A timeout leaves
-// bar[0] counting the arrivals of an abandoned barrier, so once bar[2] is set every later
-// chain on the ctx exits at entry and a late block exits before arriving; the host clears the
-// three words when it reports the timeout (nic_capi.hip chain_timeout_check: device idle).
-constexpr unsigned long long kBarrierTimeoutTicks = 200000000ull;
-__device__ __forceinline__ bool chain_timed_out(const int* bar) {
-  return __hip_atomic_load(bar + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-}
-__device__ __forceinline__ bool grid_barrier(int* bar, int nb, unsigned long long ticks) {
-  __shared__ int ok;
-  __syncthreads();
+// stage s's words: q[s] = next tile, q[kChainMax + s] = tiles done, q[2 kChainMax] = blocks out
+__device__ __forceinline__ void chain_stage_done(int* done, int ran) {
+  __syncthreads();  // every wave's stores of the stage are issued and waited for
   if (threadIdx.x == 0) {
-    ok = 1;
-    const int gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();  // release this block's stage outputs
-    if (chain_timed_out(bar)) {
-      ok = 0;  // the barrier was abandoned before this block arrived
-    } else if (atomicAdd(bar, 1) == nb - 1) {
-      __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
-      atomicAdd(bar + 1, 1);
-    } else {
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-          atomicExch(bar + 2, 1);  // vector atomic
-          ok = 0;
-          break;
-        }
-      }
-    }
-    __threadfence();  // acquire the other blocks' outputs
+    __threadfence();  // release them device-wide (every XCD)
+    if (ran) atomicAdd(done, ran);
+  }
+}
+__device__ __forceinline__ void chain_stage_wait(const int* done, int total) {
+  if (threadIdx.x == 0) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) __builtin_amdgcn_s_sleep(2);
+    __threadfence();  // acquire the other blocks' stage outputs
   }
   __syncthreads();
-  return ok != 0;
 }
 
 __global__ __launch_bounds__(256, 2) void fp32_chain_kernel(Fp32Chain ch) {
   KT_SCOPE(4);
   __shared__ __attribute__((aligned(16))) float lds[kChainLds];
   if (range_gated_off(ch.gate)) return;  // whole grid: the gate word is the same for every block
-  if (chain_timed_out(ch.bar)) return;   // an earlier chain on this ctx timed out (not yet reported)
   const int b0 = blockIdx.x, nb = gridDim.x;
+  int* q = ch.q;
+  if (ch.diag_late && b0 == 0) {  // diagnostic: block 0 starts ~1 ms late
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 100000ull) __builtin_amdgcn_s_sleep(8);
+  }
   for (int s = 0; s < ch.nstage; ++s) {
-    if (s > 0 && ch.diag_skip && b0 == nb - 1) return;  // diagnostic: this block never arrives
-    if (s > 0 && !grid_barrier(ch.bar, nb, ch.timeout_ticks)) return;
+    if (s > 0) chain_stage_wait(q + kChainMax + s - 1, ch.total[s - 1]);
     const ConvArgs& a = ch.c[s];
+    int* qs = q + s;
+    int ran = 0;
     switch (ch.kind[s]) {
-      case L_CONV1: conv1_colour_body(ch.c1, lds, b0, nb); break;
-      case L_DCONV8: dconv8_colour_body<1>(ch.d8, lds, b0, nb); break;
-      case L_CONV2: conv_mfma_body<32, 64, 5, 2, false, 8, 8, 2, 2, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_CONV1: ran = conv1_colour_body(ch.c1, lds, b0, nb, qs); break;
+      case L_DCONV8: ran = dconv8_colour_body<1>(ch.d8, lds, b0, nb, qs); break;
+      case L_CONV2: ran = conv_mfma_body<32, 64, 5, 2, false, 8, 8, 2, 2, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb, qs); break;
       case L_CONV3:
-      case L_DCONV5: conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_DCONV5: ran = conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb, qs); break;
       case L_CONV4:
-      case L_DCONV6: conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, lds, b0, nb); break;
-      case L_CONV8: conv_mfma_body<64, 32, 5, 2, false, 4, 8, 1, 1, 4, IN_F32, OUT_U8_LATENT, false>(a, lds, b0, nb); break;
-      case L_DCONV1: conv_mfma_body<32, 64, 5, 2, true, 8, 8, 2, 2, 1, IN_U8_LATENT, OUT_F32, false>(a, lds, b0, nb); break;
-      case L_DCONV7: conv_mfma_body<64, 64, 5, 2, true, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb); break;
+      case L_DCONV6: ran = conv_mfma_body<64, 64, 3, 1, false, 8, 16, 4, 1, 1, IN_F32, OUT_F32, true>(a, lds, b0, nb, qs); break;
+      case L_CONV8: ran = conv_mfma_body<64, 32, 5, 2, false, 4, 8, 1, 1, 4, IN_F32, OUT_U8_LATENT, false>(a, lds, b0, nb, qs); break;
+      case L_DCONV1: ran = conv_mfma_body<32, 64, 5, 2, true, 8, 8, 2, 2, 1, IN_U8_LATENT, OUT_F32, false>(a, lds, b0, nb, qs); break;
+      case L_DCONV7: ran = conv_mfma_body<64, 64, 5, 2, true, 8, 16, 4, 1, 1, IN_F32, OUT_F32, false>(a, lds, b0, nb, qs); break;
       default: break;
     }
+    chain_stage_done(q + kChainMax + s, ran);
+  }
+  if (threadIdx.x == 0 && atomicAdd(q + 2 * kChainMax, 1) == nb - 1) {  // the last block out: reset
+    for (int s = 0; s < ch.nstage; ++s) {
+      __hip_atomic_store(q + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + kChainMax + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(q + 2 * kChainMax, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -4637,7 +4652,9 @@ static void conv_tiles(LayerId id, ConvArgs& a) {  // launch_conv's tile grid fo
 hipError_t chain_add_layer(Fp32Chain& ch, LayerId id, ConvArgs a) {
   if (ch.nstage >= kChainMax || id == L_CONV1 || id == L_DCONV8 || id >= L_COUNT) return hipErrorInvalidValue;
   conv_tiles(id, a);
-  if ((long long)a.tiles_y * a.tiles_x * a.P > INT32_MAX) return hipErrorInvalidValue;
+  // < INT32_MAX - grid: the queue word counts past the total by at most one take per block
+  if ((long long)a.tiles_y * a.tiles_x * a.P > INT32_MAX / 2) return hipErrorInvalidValue;
+  ch.total[ch.nstage] = a.tiles_y * a.tiles_x * a.P;
   ch.kind[ch.nstage] = id;
   ch.c[ch.nstage++] = a;
   return hipSuccess;
@@ -4647,6 +4664,8 @@ hipError_t chain_add_conv1(Fp32Chain& ch, Conv1Args a) {
   if (ch.nstage >= kChainMax) return hipErrorInvalidValue;
   a.tiles_y = (a.OH + C1_T - 1) / C1_T;
   a.tiles_x = (a.OW + C1_T - 1) / C1_T;
+  if ((long long)a.tiles_y * a.tiles_x * a.P > INT32_MAX / 2) return hipErrorInvalidValue;
+  ch.total[ch.nstage] = a.tiles_y * a.tiles_x * a.P;
   ch.kind[ch.nstage++] = L_CONV1;
   ch.c1 = a;
   return hipSuccess;
@@ -4656,12 +4675,15 @@ hipError_t chain_add_dconv8(Fp32Chain& ch, Dconv8Args a) {
   if (ch.nstage >= kChainMax) return hipErrorInvalidValue;
   a.tiles_y = (a.H + D8_TH - 1) / D8_TH;
   a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
+  if ((long long)a.tiles_y * a.tiles_x * a.nimg > INT32_MAX / 2) return hipErrorInvalidValue;
+  ch.total[ch.nstage] = a.tiles_y * a.tiles_x * a.nimg;
   ch.kind[ch.nstage++] = L_DCONV8;
   ch.d8 = a;
   return hipSuccess;
 }
 
-// Blocks of fp32_chain_kernel resident per CU (its LDS / VGPRs; >= 1 required), per device.
+// Blocks of fp32_chain_kernel resident per CU (its LDS / VGPRs), per device (informational:
+// the queued chain runs on any number of resident blocks).
 static int chain_occupancy() {
   static int cache[64] = {};
   int d = 0;
@@ -4674,60 +4696,31 @@ static int chain_occupancy() {
   return cache[d];
 }
 
-// NIC_COOP=1 forces the cooperative launch of the chained re-run, NIC_COOP=0 the plain one
-// (A/B); default: plain when two chains fit per CU (see launch_fp32_chain)
-static int chain_coop_switch() {
+// NIC_DIAG_CHAIN=N (GPU test only): the chain's grid is N blocks per CU -- far more than fit at
+// once, so most blocks start only after others have left -- and block 0 starts ~1 ms late
+static int chain_diag_grid() {
   static const int v = [] {
-    const char* e = getenv("NIC_COOP");
-    return !e ? -1 : e[0] == '0' ? 0 : 1;
+    const char* e = getenv("NIC_DIAG_CHAIN");
+    return e ? std::max(1, std::min(64, atoi(e))) : 0;
   }();
   return v;
 }
 
 void fp32_chain_launch_info(int* blocks_per_cu, int* grid, int* cooperative) {
-  const int occ = chain_occupancy();
-  const int sw = chain_coop_switch();
-  *blocks_per_cu = occ;
-  *grid = device_cus();
-  *cooperative = (sw == 1 || (sw < 0 && occ < 2)) ? 1 : 0;
-}
-
-// NIC_DIAG_BARRIER=skip: the grid's last block never arrives at the chain's barriers and the
-// wait is cut to ~1 ms, so a tripped pass exercises the timeout path (GPU test only)
-static bool chain_diag_skip() {
-  static const bool v = [] {
-    const char* e = getenv("NIC_DIAG_BARRIER");
-    return e && strcmp(e, "skip") == 0;
-  }();
-  return v;
+  *blocks_per_cu = chain_occupancy();
+  *grid = device_cus() * std::max(1, chain_diag_grid());
+  *cooperative = 0;
 }
 
 hipError_t launch_fp32_chain(const Fp32Chain& chain, hipStream_t st) {
   if (chain.nstage == 0) return hipSuccess;
-  if (!chain.bar || !chain.gate.gate) return hipErrorInvalidValue;
+  if (!chain.q || !chain.gate.gate) return hipErrorInvalidValue;
+  if (chain_occupancy() < 1) return hipErrorInvalidConfiguration;
   Fp32Chain ch = chain;
-  ch.diag_skip = chain_diag_skip() ? 1 : 0;
-  ch.timeout_ticks = ch.diag_skip ? 100000ull : kBarrierTimeoutTicks;
-  // One 256-thread block per CU; the grid barrier needs every block resident at once.
-  // occupancy >= 1 makes that possible on an idle device.  Kernels of other streams only
-  // delay blocks (they finish without waiting on the chain); what could deadlock is two
-  // chains (two contexts tripping at once) splitting the CUs.  The chain's LDS (49 KB) and
-  // VGPRs allow 3 blocks per CU, so with occupancy >= 2 two chains are co-resident and the
-  // plain launch is safe.  Below that the cooperative launch guarantees co-residency.  It
-  // is not the default: the runtime serialises a cooperative dispatch against the other
-  // streams -- the three-stream host-array surface fell from 1,977 to 1,411 MP/s -- and
-  // under rocprofv3 the process then segfaults in exit() after the profiler's finalisation
-  // (profiles/r3a_coop_rocprof_exit_crash.txt: the kernel trace is complete; the fault is
-  // in the runtime's atexit teardown).  The barrier's bounded wait catches anything else.
-  const int occ = chain_occupancy();
-  if (occ < 1) return hipErrorInvalidConfiguration;
-  const dim3 grid(device_cus()), block(256);
-  const int sw = chain_coop_switch();
-  if (sw == 1 || (sw < 0 && occ < 2)) {
-    void* args[] = {const_cast<Fp32Chain*>(&ch)};
-    return hipLaunchCooperativeKernel((const void*)fp32_chain_kernel, grid, block, args, 0, st);
-  }
-  hipLaunchKernelGGL(fp32_chain_kernel, grid, block, 0, st, ch);
+  const int diag = chain_diag_grid();
+  ch.diag_late = diag ? 1 : 0;
+  // one 256-thread block per CU; nothing requires them resident together
+  hipLaunchKernelGGL(fp32_chain_kernel, dim3(device_cus() * std::max(1, diag)), dim3(256), 0, st, ch);
   return hipGetLastError();
 }
 

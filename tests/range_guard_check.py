@@ -1,6 +1,7 @@
 """Child-process run of the f16 range-guard contract (tests/test_gpu_parity.py
 range_guard_contract) under a load-time switch: NIC_CHAIN=0 (the gated exact-fp32 re-run as
-one launch per layer) or NIC_COOP=1 (the chained re-run as a cooperative launch).  Run by
+one launch per layer) or NIC_DIAG_CHAIN=N (the chained re-run on N blocks per CU, block 0
+started late: no co-residency).  Run by
 test_gpu_parity.py::test_f16_range_guard_rerun_variants; prints RANGE-OK."""
 import os
 import sys
@@ -17,7 +18,7 @@ from test_gpu_parity import range_guard_contract  # noqa: E402
 
 
 def main():
-    assert os.environ.get("NIC_CHAIN") == "0" or os.environ.get("NIC_COOP") == "1"
+    assert os.environ.get("NIC_CHAIN") == "0" or os.environ.get("NIC_DIAG_CHAIN")
     range_guard_contract(load_case, W.seeded_weights(0, init="spread"))
     print("RANGE-OK")
 
