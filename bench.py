@@ -546,11 +546,9 @@ def main():
     geo = layer_geometry(H, W)
     layers = {}
     conv1_fused = lt["conv1"][1] == 0 and lt["conv2"][1] > 0  # f16x3: conv1 runs inside conv2's kernel
-    # f16x3 with the weight-stationary kernels: dconv8's MACs run inside dconv7's kernel (the
-    # per-pixel tap projections); the dconv8 launch is then an HBM-bound gather (the library's
-    # rule, csrc/nic_kernels.hip dconv78_fused)
-    d78_fused = (args.precision == "f16x3" and os.environ.get("NIC_WS", "1")[:1] != "0"
-                 and os.environ.get("NIC_D8", "p")[:1] not in ("t", "s"))
+    # f16x3: dconv8's MACs run inside dconv7's kernel (the per-pixel tap projections); the
+    # dconv8 launch is then an HBM-bound gather (csrc/nic_capi.hip decode_pass)
+    d78_fused = args.precision == "f16x3"
     moved = {"conv2": "conv1" if conv1_fused else None, "dconv7": "dconv8" if d78_fused else None}
     # the fused k3 residual pairs (planes up to 64 columns): one launch each, timed as conv4 / dconv6
     k3_fused = {"conv4": "conv3", "dconv6": "dconv5"}

@@ -662,7 +662,7 @@ namespace {
 bool use_k3pair() {
   static const bool on = [] {
     const char* e = getenv("NIC_K3P");
-    return !(e && e[0] == '0') && conv12_fused();  // conv12_fused(): the weight-stationary set (NIC_WS)
+    return !(e && e[0] == '0');
   }();
   return on;
 }
@@ -723,7 +723,7 @@ int encode_pass(nic_ctx* c, const uint8_t* rgb, int n, int h, int w, uint8_t* la
   chain.gate = rg;
   chain.q = c->range + 2;
   // f16x3: conv1 runs inside the conv2 kernel (launch_conv12_x3, timed as conv2)
-  const bool fuse12 = x3 && conv12_fused();
+  const bool fuse12 = x3;
   if (!fuse12) TIMED(L_CONV1, chained ? chain_add_conv1(chain, a1) : launch_conv1(a1, st));
   // the re-run's head is conv1 (it counts the trip); later layers only gate
   RangeGuard rgl = rg;
@@ -857,7 +857,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
   }
   ConvArgs d7 = conv(L_DCONV7, R[3], R[0], nullptr, h2, w2, 2 * h2, 2 * w2);
   // f16x3: dconv7 writes dconv8's per-pixel tap projections (100 B / pixel instead of 256)
-  const bool fuse78 = x3 && dconv78_fused();
+  const bool fuse78 = x3;
   if (fuse78) {
     d7.proj = R[0];
     d7.proj_w = c->wproj;
@@ -888,7 +888,7 @@ int decode_pass(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, uint8_
     a8.tiles_x7 = (w2 + 7) / 8;
     TIMED(L_DCONV8, launch_dconv8_gather(a8, st));
   } else {
-    TIMED(L_DCONV8, x3 ? launch_dconv8_x3(a8, st) : chained ? chain_add_dconv8(chain, a8) : launch_dconv8(a8, st));
+    TIMED(L_DCONV8, chained ? chain_add_dconv8(chain, a8) : launch_dconv8(a8, st));
   }
   if (chained) HIP_TRY(launch_fp32_chain(chain, st));
   return NIC_OK;
@@ -934,18 +934,14 @@ int guarded(nic_ctx* c, hipStream_t st, const char* what, bool x3_fits, Pass pas
 // Chunk k of a host call: its H2D DMA on hs[0], its device pass on hs[1], its D2H DMA on hs[2],
 // so chunk k+1's copy-in and chunk k-1's copy-out overlap chunk k's pass.  Chunk sizes ramp
 // up and down (weights min(2^i, 2^(K-1-i))): a small first chunk starts the device early and
-// a small last chunk keeps the exposed D2H tail short.
-// NIC_HOST_EDGE=e (A/B): first and last chunk e/1000 of a middle chunk, the middle ones equal.
+// a small last chunk keeps the exposed D2H tail short (edge chunks at 0.25 / 0.35 of a middle
+// one and equal middles measured the same, round 4).
 void host_chunk_plan(int n, int k, std::vector<int>& lo) {
-  static const int edge = [] {
-    const char* e = getenv("NIC_HOST_EDGE");
-    return e ? std::max(1, std::min(4000, atoi(e))) : 0;
-  }();
   k = std::max(1, std::min({k, n, kHostMaxChunks}));
   std::vector<double> wgt(k);
   double tot = 0;
   for (int i = 0; i < k; ++i)
-    tot += wgt[i] = edge && k >= 3 ? (i == 0 || i == k - 1 ? edge / 1000.0 : 1.0) : (double)(1 << std::min(i, k - 1 - i));
+    tot += wgt[i] = (double)(1 << std::min(i, k - 1 - i));
   lo.assign(1, 0);
   double acc = 0;
   for (int i = 0; i < k; ++i) {
@@ -1057,15 +1053,9 @@ class CopyPool {
 // tails, measured slower in round 4 -- round trip 2.15-2.20 vs 1.93-1.96 ms: two chunk passes'
 // persistent kernels, one block per CU each, contend for the CUs -- and was removed.)
 
-// Host-side wait for an event: polling hipEventQuery (default) returns as soon as the GPU
-// signals, where hipEventSynchronize may sleep and pay a wake-up latency per chunk
-// (NIC_HOST_SPIN=0 for the runtime's wait).
+// Host-side wait for an event: polling hipEventQuery returns as soon as the GPU signals, where
+// hipEventSynchronize may sleep and pay a wake-up latency per chunk (no worse, less jitter).
 hipError_t host_wait(hipEvent_t e) {
-  static const bool spin = [] {
-    const char* v = getenv("NIC_HOST_SPIN");
-    return !(v && v[0] == '0');
-  }();
-  if (!spin) return hipEventSynchronize(e);
   for (;;) {
     const hipError_t r = hipEventQuery(e);
     if (r != hipErrorNotReady) return r;
@@ -1257,7 +1247,7 @@ int nic_entropy_hist(nic_ctx* c, const uint8_t* latent, int n, int h8, int w8, u
 // per block of its group (hist_fold_supported); otherwise nic_encode_entropy runs the two calls
 static bool encode_entropy_folds(const nic_ctx* c, int n, int h, int w) {
   const EncGeom eg = enc_geom(n, h, w);
-  return c->precision == NIC_PRECISION_F16X3 && x3_plane_fits(eg.c2y.out, eg.c2x.out) && conv12_fused() &&
+  return c->precision == NIC_PRECISION_F16X3 && x3_plane_fits(eg.c2y.out, eg.c2x.out) &&
          hist_fold_supported(n, eg.c8y.out, eg.c8x.out);
 }
 

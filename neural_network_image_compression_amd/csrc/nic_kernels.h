@@ -58,11 +58,9 @@ struct ConvArgs {
   int ws_ngrp;            // weight-stationary kernels: block groups (tap set x model)
   int ws_blk[9];          // weight-stationary kernels: first block of each group, then the grid
   int ws_xcd;             // weight-stationary kernels: logical block = XCD-contiguous remap of blockIdx
-  int tile_xcd;           // k5 s2 tap-split kernels: XCD-contiguous tile positions (xcd_pos)
   // conv8 (f16x3, OUT_U8_LATENT) with the latent histogram folded in (nic_encode_entropy):
   // the counts [3 nimg][256], zero on entry, added to with device-scope atomics
   uint32_t* hist_part;
-  int ws2_xrange;         // A/B (NIC_C8W=x): conv8 without the fold on the fold's XCD-range tile walk
   // fused k3 residual pair (conv3 -> conv4 -> + x, dconv5 -> dconv6 -> + x): the second
   // layer's weights (wx / wscale / bias are the first layer's), rows per block segment
   const uint16_t* wx2;
@@ -108,7 +106,6 @@ struct Dconv8Args {
   float wscale[2];      // f16x3 path: 2^-k per model
   const float* bias;    // [2]
   int nimg, H, W, tiles_x, tiles_y;
-  int strips, nseg, seg_rows;  // strip-walk kernel: column strips, row segments
   const float* proj;           // gather kernel: dconv7's projections (ConvArgs::proj layout)
   int tiles_y7, tiles_x7;      // gather kernel: dconv7's 8x8 tile grid over its coarse input
 };
@@ -145,13 +142,10 @@ hipError_t launch_conv12_x3(const ConvArgs& a, hipStream_t st);  // conv1 fused 
 // the fused conv1's padded colour planes: origin offsets and plane size in f16 elements
 // (a.cplane must hold 2 * P * hp * wp of them)
 void c12_plane_geom(int OH, int OW, int pad_y, int pad_x, int p1y, int p1x, int* oy, int* ox, int* hp, int* wp);
-bool conv12_fused();  // whether nic_encode uses launch_conv12_x3 in f16x3 mode
 hipError_t launch_conv1(Conv1Args a, hipStream_t st);
 hipError_t launch_dconv8(Dconv8Args a, hipStream_t st);      // exact fp32 VALU
-hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st);   // split-f16 MFMA
 // f16x3 decoder tail with dconv8 split across two kernels: dconv7 writes the 25 projections
 // of every output pixel instead of its 64 channels, the gather sums them per output pixel
-bool dconv78_fused();
 hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st);
 hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st);
 // histogram entropy: per-block partial counts into `part` (hist_scratch_bytes), then one

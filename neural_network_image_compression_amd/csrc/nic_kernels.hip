@@ -470,68 +470,6 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
-// NIC_PIN=1: scheduling fences so that prefetch loads (next tap's B fragments from L2, next
-// k-step's A fragments from LDS) issue before the MFMA block they overlap with; without
-// them hipcc sinks the global loads to the loop back-edge (their latency then lands on
-// the next tap's first MFMA).
-#ifndef NIC_PIN
-#define NIC_PIN 1
-#endif
-// NIC_DMA_STAGE=1: one-tile-per-block kernels stage split halos by LDS-DMA instead of VGPRs
-#ifndef NIC_DMA_STAGE
-#define NIC_DMA_STAGE 0
-#endif
-#if NIC_PIN
-#define NIC_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define NIC_FENCE() \
-  do {              \
-  } while (0)
-#endif
-
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, bool LO = true>
-struct GeomX3 {
-  static constexpr int NWAVES = WM * WN * WK;
-  static constexpr int NTHREADS = 64 * NWAVES;
-  static_assert(CIN % 16 == 0 && COUT % 32 == 0, "channel tiling");
-  static constexpr int MT = TH * TW / 32;
-  static_assert(MT == WM * MTW && (TH * TW) % 32 == 0, "M tiling");
-  static_assert(TW == 8 || TW == 16 || TW % 32 == 0, "M tile = 32 pixels of 4x8, 2x16 or 1x32");
-  static constexpr int NT = COUT / 32;
-  static_assert(NT % WN == 0, "N tiling");
-  static constexpr int NTW = NT / WN;
-  static constexpr int HH = TR ? TH + 2 : (TH - 1) * S + KS;
-  static constexpr int HW = TR ? TW + 2 : (TW - 1) * S + KS;
-  // LDS bytes per halo pixel: [hi | lo | pad], or [hi | pad] for exact f16 operands (no
-  // lo half: IN_U8_CODES); an odd number of 16-B slots
-  static constexpr int PSB = CIN * (LO ? 4 : 2) + 16;
-  static_assert((PSB / 16) % 2 == 1, "pixel stride must be an odd slot count");
-  static constexpr int NS = CIN / 16;       // k16 steps per tap
-  static constexpr int NTAPS = KS * KS;
-  // Stride-2 forward convs store even halo columns first, then odd ones, so that the 32
-  // lanes of an M tile read consecutive stored pixels for every tap.
-  static constexpr bool S2 = !TR && S == 2;
-  static constexpr int HE = S2 ? (HW + 1) / 2 : HW;
-  // Halo row pitch (16-B slots), padded so that the pitch between the rows of one M tile
-  // is 0 (TW = 16) or 8 (TW = 8) mod 16 slots: each 16-lane ds_read_b128 group then
-  // touches 16 distinct slots of the 64-bank row (conflict-free A-fragment reads).
-  static constexpr int MP_MOD = TW == 16 ? 0 : TW == 8 ? 8 : -1;
-  static constexpr int rps() {
-    int r = HW * (PSB / 16);
-    if (MP_MOD < 0) return r;
-    while (((S2 ? 2 : 1) * r) % 16 != MP_MOD) ++r;
-    return r;
-  }
-  static constexpr int RPB = rps() * 16;  // bytes per halo row
-  // DMA staging writes whole 64-slot wave-instructions: round the image up to them
-  static constexpr int HALO_BYTES = (HH * RPB + 1023) / 1024 * 1024;
-  static constexpr int RED_BYTES = (WK > 1) ? (WK - 1) * WM * WN * MTW * NTW * 1024 * 4 : 0;
-  static constexpr int LDS_BYTES = HALO_BYTES > RED_BYTES ? HALO_BYTES : RED_BYTES;
-  // LDS byte offset of halo pixel (hy, hx)
-  static __device__ __forceinline__ int pix_off(int hy, int hx) {
-    return hy * RPB + (S2 ? ((hx & 1) * HE + (hx >> 1)) : hx) * PSB;
-  }
-};
 
 #ifndef NIC_MIX_SPLIT
 #define NIC_MIX_SPLIT 1
@@ -543,19 +481,24 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x4& hi, f16x4& lo) {
   // them.  v - f32(hi) is exact in fp32 (Sterbenz; hi within 2x of v or both tiny), so this
   // is bit-identical to (_Float16)(v - (float)(_Float16)v) (checked over 16M values,
   // tools/mixcheck.hip).
+  // One asm block for the 8 instructions, each result read at least one instruction after it
+  // is written: as separate statements the compiler cannot see that none of them is a
+  // transcendental op and pads every dependent pair with an s_nop (2-3 per call).
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   u32x2 H, L;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    unsigned h, l;
-    float d0, d1;
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(v[2 * k]), "v"(v[2 * k + 1]));
-    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(h), "v"(v[2 * k]));
-    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(h), "v"(v[2 * k + 1]));
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(d0), "v"(d1));
-    H[k] = h;
-    L[k] = l;
-  }
+  float d0, d1, d2, d3;
+  asm("v_cvt_pk_f16_f32 %0, %6, %7\n\t"
+      "v_cvt_pk_f16_f32 %1, %8, %9\n\t"
+      "v_fma_mix_f32 %2, -%0, 1.0, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, -%0, 1.0, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %4, -%1, 1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %5, -%1, 1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(H[0]), "=&v"(H[1]), "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+  asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_cvt_pk_f16_f32 %1, %4, %5"
+      : "=&v"(L[0]), "=&v"(L[1])
+      : "v"(d0), "v"(d1), "v"(d2), "v"(d3));
   hi = __builtin_bit_cast(f16x4, H);
   lo = __builtin_bit_cast(f16x4, L);
 #else
@@ -607,465 +550,9 @@ __device__ __forceinline__ void swap_pair(f16x4& a, f16x4& b) {
   b = __builtin_bit_cast(f16x4, ub);
 }
 
-// Stage a split-format halo by DMA: every 16-B slot of the LDS image (pixel records of
-// PSB bytes, padded rows) is one lane-load; record slot k < Cin/4 copies slot k of the
-// pixel's [hi | lo] record in HBM, the pad slot, row padding and out-of-image pixels load
-// zeros.  One HBM round trip per block, no VGPR staging, no conversion.
-template <class G, int CIN>
-__device__ __forceinline__ void stage_halo_dma(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
-  constexpr int PSS = G::PSB / 16, RPS = G::RPB / 16;
-  constexpr int TOTAL = G::HH * RPS;
-  const char* base = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-#pragma unroll 4
-  for (int q0 = wave * 64; q0 < TOTAL; q0 += G::NTHREADS) {
-    const int q = q0 + lane;
-    const int row = q / RPS, r = q - row * RPS;
-    const int sp = r / PSS, k = r - sp * PSS;
-    const int hx = G::S2 ? (sp < G::HE ? 2 * sp : 2 * (sp - G::HE) + 1) : sp;
-    const int gy = gy0 + row, gx = gx0 + hx;
-    const bool valid = q < TOTAL && sp < G::HW && k < PSS - 1 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-    const char* src = valid ? base + ((size_t)gy * a.W + gx) * (CIN * 4) + k * 16 : a.zero16;
-    dma16(src, lds + q0 * 16);
-  }
-}
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Split-format halo through VGPRs: the LDS record [hi Cin | lo Cin | pad] starts with the
-// HBM record [hi Cin | lo Cin], so staging is a 16-B copy per (pixel, slot); batches of 16
-// clamped loads are in flight before the first LDS write, out-of-image pixels write zeros.
-template <class G, int CIN>
-__device__ __forceinline__ void stage_halo_split(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
-  constexpr int C4 = CIN / 4;  // 16-B slots per pixel record in HBM
-  constexpr int TOTAL = G::HH * G::HW * C4;
-  constexpr int ITER = (TOTAL + G::NTHREADS - 1) / G::NTHREADS;
-  constexpr int BATCH = 16;
-  const char* inb = (const char*)a.in_s + (size_t)p * a.H * a.W * CIN * 4;
-#pragma unroll
-  for (int it0 = 0; it0 < ITER; it0 += BATCH) {
-    u32x4 v[BATCH];
-    bool inside[BATCH];
-#pragma unroll
-    for (int b = 0; b < BATCH; ++b) {
-      if (it0 + b >= ITER) break;
-      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
-      const int pix = idx / C4, k = idx - pix * C4;
-      const int hy = pix / G::HW, hx = pix - hy * G::HW;
-      const int gy = gy0 + hy, gx = gx0 + hx;
-      inside[b] = idx < TOTAL && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-      const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-      v[b] = *(const u32x4*)(inb + ((size_t)cy * a.W + cx) * (CIN * 4) + k * 16);
-    }
-#pragma unroll
-    for (int b = 0; b < BATCH; ++b) {
-      if (it0 + b >= ITER) break;
-      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
-      if (idx < TOTAL) {
-        const int pix = idx / C4, k = idx - pix * C4;
-        const int hy = pix / G::HW, hx = pix - hy * G::HW;
-        *(u32x4*)(lds + G::pix_off(hy, hx) + k * 16) = inside[b] ? v[b] : (u32x4){0u, 0u, 0u, 0u};
-      }
-    }
-  }
-}
-
-template <class G, int IN_MODE, int CIN>
-__device__ __forceinline__ void stage_halo_x3(char* lds, const ConvArgs& a, int p, int gy0, int gx0) {
-  constexpr int C4 = CIN / 4;
-  constexpr int TOTAL = G::HH * G::HW * C4;
-  constexpr int ITER = (TOTAL + G::NTHREADS - 1) / G::NTHREADS;
-  constexpr int BATCH = 16;
-  const float* inp = nullptr;
-  const uint8_t* inq = nullptr;
-  if constexpr (IN_MODE == IN_F32) {
-    inp = a.in + (size_t)p * a.H * a.W * CIN;
-  } else {
-    static_assert(CIN == 32, "latent planes carry 32 channels");
-    inq = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
-  }
-#pragma unroll
-  for (int it0 = 0; it0 < ITER; it0 += BATCH) {
-    f32x4 v[BATCH];
-    bool inside[BATCH];
-#pragma unroll
-    for (int b = 0; b < BATCH; ++b) {
-      if (it0 + b >= ITER) break;
-      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
-      const int pix = idx / C4, c4 = idx - pix * C4;
-      const int hy = pix / G::HW, hx = pix - hy * G::HW;
-      const int gy = gy0 + hy, gx = gx0 + hx;
-      inside[b] = idx < TOTAL && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-      const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-      if constexpr (IN_MODE == IN_F32) {
-        v[b] = *(const f32x4*)(inp + ((size_t)cy * a.W + cx) * CIN + c4 * 4);
-      } else if constexpr (IN_MODE == IN_U8_CODES) {
-        const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
-        v[b][0] = __builtin_bit_cast(float, q);  // raw bytes; converted to f16 codes at the store
-      } else {
-        const uint32_t q = *(const uint32_t*)(inq + ((size_t)cy * a.W + cx) * 96 + c4 * 4);
-        v[b][0] = u8_unit(q & 255);  // in registers: no table load per byte
-        v[b][1] = u8_unit((q >> 8) & 255);
-        v[b][2] = u8_unit((q >> 16) & 255);
-        v[b][3] = u8_unit(q >> 24);
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < BATCH; ++b) {
-      if (it0 + b >= ITER) break;
-      const int idx = threadIdx.x + (it0 + b) * G::NTHREADS;
-      if (idx < TOTAL) {
-        const int pix = idx / C4, c4 = idx - pix * C4;
-        const int hy = pix / G::HW, hx = pix - hy * G::HW;
-        char* d = lds + G::pix_off(hy, hx) + c4 * 8;
-        if constexpr (IN_MODE == IN_U8_CODES) {
-          // codes 0..255 are exact in f16: (float)byte -> f16, no split
-          const uint32_t q = inside[b] ? __builtin_bit_cast(uint32_t, v[b][0]) : 0u;
-          const f16x4 c = {(_Float16)(float)(q & 255), (_Float16)(float)((q >> 8) & 255),
-                           (_Float16)(float)((q >> 16) & 255), (_Float16)(float)(q >> 24)};
-          *(f16x4*)d = c;
-        } else {
-          f32x4 x = v[b];
-          if (!inside[b]) x = (f32x4){0.f, 0.f, 0.f, 0.f};
-          f16x4 hi, lo;
-          split4(x, hi, lo);
-          *(f16x4*)d = hi;
-          *(f16x4*)(d + CIN * 2) = lo;
-        }
-      }
-    }
-  }
-}
-
-template <int NS, int NTW, int COUT>
-__device__ __forceinline__ void load_b_x3(f16x8 (&b)[NS][2][NTW], const char* wt, int wn) {
-  // wt: this lane's base for one tap: + (((s*2 + hl)*2 + h)*COUT + co)*16 bytes
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        b[s][hl][j] = *(const f16x8*)(wt + ((s * 2 + hl) * 2 * COUT + (wn * NTW + j) * 32) * 16);
-}
-
-template <int MTW, int CIN, bool LO = true>
-__device__ __forceinline__ void load_a_x3(f16x8 (&ahi)[MTW], f16x8 (&alo)[MTW], const char* lds, const int (&a_off)[MTW],
-                                          int off) {
-#pragma unroll
-  for (int i = 0; i < MTW; ++i) {
-    ahi[i] = *(const f16x8*)(lds + a_off[i] + off);
-    if constexpr (LO) alo[i] = *(const f16x8*)(lds + a_off[i] + off + CIN * 2);
-  }
-}
-
-// One tap: NS k16 steps x MTW x NTW tiles x 3 MFMAs.  The weights are the MFMA A operand
-// (rows = output channels) and the activations the B operand (columns = pixels), so the
-// accumulator holds D[co][pixel]: each lane owns one pixel and, per register group g, four
-// consecutive channels -- the epilogue then writes 16-B vectors.  A fragments are double
-// buffered: step s+1 (or step 0 of the next tap, at offset toff_next) is read while the
-// MFMAs of step s run.
-// LO = false: the activation is exact in f16 (u8 codes), its lo half is zero -- 2 MFMAs.
-template <int MTW, int NTW, int NS, int CIN, bool LO = true>
-__device__ __forceinline__ void mma_tap_x3(f32x16 (&acc)[MTW][NTW], const f16x8 (&b)[NS][2][NTW], const char* lds,
-                                           const int (&a_off)[MTW], int toff, int toff_next, f16x8 (&ahi0)[MTW],
-                                           f16x8 (&alo0)[MTW]) {
-  f16x8 ahi1[MTW], alo1[MTW];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    f16x8(&chi)[MTW] = (s & 1) ? ahi1 : ahi0;
-    f16x8(&clo)[MTW] = (s & 1) ? alo1 : alo0;
-    f16x8(&nhi)[MTW] = (s & 1) ? ahi0 : ahi1;
-    f16x8(&nlo)[MTW] = (s & 1) ? alo0 : alo1;
-    if (s + 1 < NS)
-      load_a_x3<MTW, CIN, LO>(nhi, nlo, lds, a_off, toff + (s + 1) * 32);
-    else
-      load_a_x3<MTW, CIN, LO>(nhi, nlo, lds, a_off, toff_next);
-    NIC_FENCE();
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][1][j], chi[i], acc[i][j], 0, 0, 0);  // w_lo*a_hi
-        if constexpr (LO)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], clo[i], acc[i][j], 0, 0, 0);  // w_hi*a_lo
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b[s][0][j], chi[i], acc[i][j], 0, 0, 0);  // w_hi*a_hi
-      }
-    NIC_FENCE();
-  }
-  if constexpr (NS % 2 == 1) {  // the next tap's step 0 landed in the odd buffer
-#pragma unroll
-    for (int i = 0; i < MTW; ++i) {
-      ahi0[i] = ahi1[i];
-      if constexpr (LO) alo0[i] = alo1[i];
-    }
-  }
-}
-
-// Epilogue of one transposed accumulator tile D[co][pixel]: this lane's pixel is (oy, ox);
-// register r holds channel nt*32 + (r&3) + 8*(r>>2) + 4*half.  Conv -> *2^-k (exact) ->
-// BiasAdd -> leaky (-> + residual | -> clip, round(x*255) into the latent layout).
-template <int COUT, int OUT_MODE, bool RESID>
-__device__ __forceinline__ void store_tile_t(const ConvArgs& a, int p, int nt, const f32x16& acc, int oy, int ox,
-                                             float scale, const f32x4 (&b)[4], float& rmax) {
-  const bool inside = oy < a.OH && ox < a.OW;
-  const int half = (threadIdx.x >> 5) & 1;
-  const size_t pix = ((size_t)p * (inside ? a.OH : 1) + (inside ? oy : 0)) * (inside ? a.OW : 1) + (inside ? ox : 0);
-  f32x4 v[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[g][q] = leaky02(scale_bias(acc[4 * g + q], scale, b[g][q]));
-  if constexpr (OUT_MODE == OUT_SPLIT) {
-    // every lane takes part in the swaps (EXEC must stay full); only in-image lanes store
-    uint16_t* base = a.out_s + pix * COUT * 2 + nt * 32;
-    const uint16_t* rbase = a.res_s + pix * COUT * 2 + nt * 32;
-    f16x8 rh[2] = {}, rl[2] = {};
-    if constexpr (RESID) {  // residual stored split: x = hi + lo; all four 16-B loads in flight
-      if (inside) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          rh[k] = *(const f16x8*)(rbase + 16 * k + 8 * half);
-          rl[k] = *(const f16x8*)(rbase + COUT + 16 * k + 8 * half);
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < 4; g += 2) {
-      const int co = 8 * g + 8 * half;  // channel block this lane stores after the swap
-      if constexpr (RESID) {  // inverse swap back to the accumulator's channel map
-        const f16x8 &r = rh[g >> 1], &q = rl[g >> 1];
-        f16x4 h0 = {r[0], r[1], r[2], r[3]}, h1 = {r[4], r[5], r[6], r[7]};
-        f16x4 l0 = {q[0], q[1], q[2], q[3]}, l1 = {q[4], q[5], q[6], q[7]};
-        swap_pair(h0, h1);
-        swap_pair(l0, l1);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          v[g][c] = __fadd_rn(v[g][c], __fadd_rn((float)h0[c], (float)l0[c]));
-          v[g + 1][c] = __fadd_rn(v[g + 1][c], __fadd_rn((float)h1[c], (float)l1[c]));
-        }
-      }
-      if (inside) {
-        range_track(rmax, v[g]);
-        range_track(rmax, v[g + 1]);
-      }
-      f16x4 h0, l0, h1, l1;
-      split4(v[g], h0, l0);
-      split4(v[g + 1], h1, l1);
-      swap_pair(h0, h1);
-      swap_pair(l0, l1);
-      if (inside) {
-        *(f16x8*)(base + co) = (f16x8){h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        *(f16x8*)(base + COUT + co) = (f16x8){l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-      }
-    }
-    return;
-  }
-  if (!inside) return;
-  f32x4 rv[4];
-  if constexpr (RESID) {  // all residual vectors in flight before the first is used
-#pragma unroll
-    for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4*)(a.res + pix * COUT + nt * 32 + 8 * g + 4 * half);
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int co = nt * 32 + 8 * g + 4 * half;
-    if constexpr (RESID) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[g][q] = __fadd_rn(v[g][q], rv[g][q]);
-    }
-    if constexpr (OUT_MODE == OUT_F32) {
-      *(f32x4*)(a.out + pix * COUT + co) = v[g];
-    } else {
-      const int n = p % a.nimg, type = p / a.nimg;
-      const size_t lo = (((size_t)n * a.OH + oy) * a.OW + ox) * 96 + type * 32 + co;
-      uint32_t packed = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[g][q] = clip01(v[g][q]);
-        packed |= (uint32_t)quant255(v[g][q]) << (8 * q);
-      }
-      *(uint32_t*)(a.out_u8 + lo) = packed;
-      if (a.out_f32_latent) *(f32x4*)(a.out_f32_latent + lo) = v[g];
-    }
-  }
-}
-
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, int IN_MODE,
-          int OUT_MODE, bool RESID>
-__global__ __launch_bounds__(64 * WM * WN * WK) void conv_x3_kernel(ConvArgs a) {
-  constexpr bool LO = IN_MODE != IN_U8_CODES;  // u8 codes: exact f16 activations, 2 MFMAs per MAC
-  using G = GeomX3<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW, LO>;
-  constexpr int NS = G::NS, NTW = G::NTW;
-  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
-
-  const int p = blockIdx.y;
-  const int tile = blockIdx.x;
-  NIC_STAMP(0);
-  const int tyi = tile / a.tiles_x;
-  const int t0y = tyi * TH, t0x = (tile - tyi * a.tiles_x) * TW;
-  const int model = p >= a.nimg ? 1 : 0;
-  int gy0, gx0;
-  if constexpr (TR) {
-    gy0 = t0y - 1;
-    gx0 = t0x - 1;
-  } else {
-    gy0 = t0y * S - a.pad_y;
-    gx0 = t0x * S - a.pad_x;
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int half = lane >> 5;
-  const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
-  const char* wbase = (const char*)a.wx + (size_t)model * G::NTAPS * CIN * COUT * 4 +
-                      (half * COUT + (lane & 31)) * 16;
-  constexpr int TAP_BYTES = CIN * COUT * 4;
-  // this lane's bias vectors (channels nt*32 + 8g + 4*half .. +3), loaded up front
-  f32x4 bias4[NTW][4];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      bias4[j][g] = *(const f32x4*)(a.bias + model * COUT + (wn * NTW + j) * 32 + 8 * g + 4 * half);
-  f16x8 bc[NS][2][NTW], bn[NS][2][NTW];
-  const int t_begin = TR ? 0 : wk * G::NTAPS / WK, t_end = TR ? 25 : (wk + 1) * G::NTAPS / WK;
-  load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t_begin * TAP_BYTES, wn);  // in flight during staging
-
-  if constexpr (IN_MODE == IN_SPLIT_DMA || (IN_MODE == IN_SPLIT && NIC_DMA_STAGE))
-    stage_halo_dma<G, CIN>(lds, a, p, gy0, gx0);
-  else if constexpr (IN_MODE == IN_SPLIT)
-    stage_halo_split<G, CIN>(lds, a, p, gy0, gx0);
-  else
-    stage_halo_x3<G, IN_MODE, CIN>(lds, a, p, gy0, gx0);
-
-  // this lane's pixel (B-operand column) in each of its M tiles
-  int a_off[MTW], my[MTW], mx[MTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i) {
-    const int m = (wm * MTW + i) * 32 + (lane & 31);
-    my[i] = m / TW;
-    mx[i] = m - my[i] * TW;
-    // tap (0,0) pixel of this lane: (my*S, mx*S); for S == 2 the even-column block keeps
-    // consecutive mx at consecutive stored pixels
-    a_off[i] = (TR || S == 1) ? G::pix_off(my[i], mx[i]) + half * 16
-                              : my[i] * 2 * G::RPB + mx[i] * G::PSB + half * 16;
-  }
-  // 2^-k undoes the weight pre-scale; with u8 codes as the activation it also carries the
-  // dequantiser's 1/255 (decoder.py:40): fma(sum, 2^-k fl(1/255), b), one rounding
-  const float scale = IN_MODE == IN_U8_CODES ? a.wscale[model] * 0.0039215688593685627f : a.wscale[model];
-  if constexpr (IN_MODE == IN_SPLIT_DMA || (IN_MODE == IN_SPLIT && NIC_DMA_STAGE))
-    dma_wait_all();  // this wave's DMAs landed; the barrier publishes all
-  __syncthreads();
-  NIC_STAMP(1);
-
-  auto tap_off = [&](int t) {
-    if constexpr (TR) {
-      // phase-major tap order (host repack): phase ph = (py, px) has 2|3 x 2|3 halo
-      // offsets (iy, ix), one nibble per tap: iy | ix << 2.  Taps 0..3: (0,0)(0,1)(1,0)(1,1);
-      // 4..9: rows 0..1 x cols 0..2; 10..15: rows 0..2 x cols 0..1; 16..24: 3x3.  The table
-      // lives in two 64-bit immediates: t is wave-uniform, so this is a few SALU shifts; an
-      // array would be a global_load_ubyte whose vmcnt wait drains the B prefetch in flight.
-      constexpr unsigned long long kTabLo = 0x6251409518405140ull, kTabHi = 0x0000000a62951840ull;
-      const int e = (int)((t < 16 ? kTabLo >> (4 * t) : kTabHi >> (4 * (t - 16))) & 15);
-      return (e & 3) * G::RPB + (e >> 2) * G::PSB;
-    } else {
-      const int kh = t / KS, kw = t - (t / KS) * KS;
-      return G::S2 ? kh * G::RPB + ((kw & 1) * G::HE + (kw >> 1)) * G::PSB : kh * G::RPB + kw * G::PSB;
-    }
-  };
-
-  f16x8 ahi[MTW], alo[MTW];
-  load_a_x3<MTW, CIN, LO>(ahi, alo, lds, a_off, tap_off(t_begin));
-
-  f32x16 acc[MTW][NTW];
-  float rmax = 0.f;  // range guard of the split output
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[i][j] = (f32x16){};
-  };
-  // Taps [tb, te): bc holds tap tb's B fragments on entry and tap te's (clamped) on exit.
-  // Two B buffers ping-pong; each tap's successor is requested before its MFMAs.
-  auto run_taps = [&](int tb, int te) {
-#pragma unroll 1
-    for (int t = tb; t < te; t += 2) {
-      const int t1 = t + 1 < t_end ? t + 1 : t_end - 1;
-      const int t2 = t + 2 < t_end ? t + 2 : t_end - 1;
-      load_b_x3<NS, NTW, COUT>(bn, wbase + (size_t)t1 * TAP_BYTES, wn);
-      NIC_FENCE();
-      mma_tap_x3<MTW, NTW, NS, CIN, LO>(acc, bc, lds, a_off, tap_off(t), tap_off(t1), ahi, alo);
-      if (t + 1 < te) {
-        load_b_x3<NS, NTW, COUT>(bc, wbase + (size_t)t2 * TAP_BYTES, wn);
-        NIC_FENCE();
-        mma_tap_x3<MTW, NTW, NS, CIN, LO>(acc, bn, lds, a_off, tap_off(t1), tap_off(t2), ahi, alo);
-      } else {
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int hl = 0; hl < 2; ++hl)
-#pragma unroll
-            for (int j = 0; j < NTW; ++j) bc[s][hl][j] = bn[s][hl][j];
-      }
-    }
-  };
-
-  if constexpr (!TR) {
-    zero_acc();
-    run_taps(t_begin, t_end);
-    if constexpr (WK > 1) {
-      __syncthreads();  // every wave is done with the halo before it is reused
-      float* red = (float*)lds;
-      const int grp = wm + WM * wn;
-      if (wk > 0) {
-#pragma unroll
-        for (int i = 0; i < MTW; ++i)
-#pragma unroll
-          for (int j = 0; j < NTW; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              red[((((wk - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane] = acc[i][j][r];
-      }
-      __syncthreads();
-      if (wk > 0) return;
-#pragma unroll
-      for (int k = 1; k < WK; ++k)
-#pragma unroll
-        for (int i = 0; i < MTW; ++i)
-#pragma unroll
-          for (int j = 0; j < NTW; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              acc[i][j][r] =
-                  __fadd_rn(acc[i][j][r], red[((((k - 1) * WM * WN + grp) * MTW + i) * NTW + j) * 1024 + r * 64 + lane]);
-    }
-    NIC_STAMP(2);
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], t0y + my[i], t0x + mx[i], scale,
-                                            bias4[j], rmax);
-    NIC_STAMP(3);
-  } else {
-    static_assert(!TR || (S == 2 && KS == 5 && WK == 1), "transposed path: k5 s2 phases, no tap split");
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int py = ph >> 1, px = ph & 1;
-      zero_acc();
-      run_taps(ph == 0 ? 0 : ph == 1 ? 4 : ph == 2 ? 10 : 16, ph == 0 ? 4 : ph == 1 ? 10 : ph == 2 ? 16 : 25);
-      if (ph == 3) NIC_STAMP(2);
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j)
-          store_tile_t<COUT, OUT_MODE, RESID>(a, p, wn * NTW + j, acc[i][j], 2 * (t0y + my[i]) + py,
-                                              2 * (t0x + mx[i]) + px, scale, bias4[j], rmax);
-    }
-    NIC_STAMP(3);
-  }
-  range_report(a.rg, rmax);
-}
 
 // ------------------------------------------------------------------------------------
 // Persistent-kernel helpers: a tile barrier that is not a memory fence, and LDS-DMA halo
@@ -1690,18 +1177,8 @@ struct GeomS2 {
   static __device__ __forceinline__ int col(int hx) { return (hx & 1) * HE + (hx >> 1); }
 };
 
-// conv1 fused into conv2 (FUSE1): per tile the 41 x 41 colour-plane patch conv1's 19 x 19
-// halo outputs need is computed from the RGB bytes (loaded into registers by the ts = 1
-// waves while the previous tile's MFMAs run), conv1 runs on the same split-f16 MFMA
-// (K = 25 taps as 15 (kh, kw pair) slots padded to 32: each lane's 8 taps are 4 8-B patch
-// reads; B = that im2col, split on the fly) and its
-// bias + leaky + split outputs land directly in the conv2 halo (zero outside conv1's output,
-// conv2's SAME padding).  The halo and the patch are single LDS buffers: each tile runs
-// [epilogue(i-1) | patch(i)] -> barrier -> conv1(i) -> barrier -> conv2 MFMAs(i).
-constexpr int C12_PH = 41;  // patch rows / cols: (19 - 1) * 2 + 5
-// patch row pitch in LDS (floats): columns 41..51 stay zero, so the tap pairs (kw 4, 5) of
-// the last column read a finite 0 for the zero weight of kw = 5
-constexpr int C12_PP = 52;
+
+constexpr int C12_PH = 41;  // conv12's colour patch rows / cols: (19 - 1) * 2 + 5
 
 // HIST (conv8 in nic_encode_entropy): the latent histogram counted inside conv8.  The ts = 0
 // epilogue stores each tile's packed codes in LDS; the ts = 1 waves (idle ~1,700 cycles per
@@ -1721,29 +1198,16 @@ constexpr int C12_PP = 52;
 #endif
 constexpr int HIST_R = 2;
 constexpr int HIST_LDS = 2 * 256 * HIST_R * 4 + 2 * 2 * 2 * 64 * 4;  // + codes [2][NCG][MT][64] (conv8)
-__host__ __device__ inline void hist_xcd_range(int rel, int nb, long long ntot, long long* start, long long* len, int* nx,
-                                               int* j) {  // A/B walk (NIC_C8W=x): one tile range per XCD
-  const int x = rel & 7, q = nb >> 3, r = nb & 7;
-  const int px = x * q + (x < r ? x : r);  // first position of XCD class x (xcd_pos)
-  *nx = q + (x < r ? 1 : 0);
-  *j = rel >> 3;
-  *start = (long long)px * ntot / nb;
-  *len = (long long)(px + *nx) * ntot / nb - *start;
-}
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool FUSE1, bool HIST = false>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, int TS, bool HIST = false>
 __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int TW = 8, MT = TH * TW / 16, NCG = COUT / 16, KST = CIN / 32, NW = NCG * NTS;
-  static_assert(!HIST || (OUT_MODE == OUT_U8_LATENT && !FUSE1), "histogram fold: conv8 only");
+  static_assert(!HIST || OUT_MODE == OUT_U8_LATENT, "histogram fold: conv8 only");
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
-  static_assert(!FUSE1 || (CIN == 32 && TH == 8 && G::HH == 19 && NTS == 2 && OUT_MODE == OUT_SPLIT),
-                "conv1 fusion is conv2's 8x8-tile form");
   constexpr int TAP_BYTES = CIN * COUT * 4;
   constexpr int NPP = (G::NPIECE + NW - 1) / NW;
   constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
-  char* part = lds + (FUSE1 ? 1 : 2) * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
-  float* plane = (float*)(part + 2 * (NTS - 1) * NCG * PART);  // FUSE1: colour-plane patch
-  float* lut = plane + C12_PH * C12_PP;                        // FUSE1: u8 -> fp32 / 255
+  char* part = lds + 2 * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % NCG;
@@ -1751,16 +1215,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   const int per_plane = a.tiles_y * a.tiles_x;
   const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
-  int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
-  int walk_b = bi, walk_n = nb;  // tile walk: start, stride
-  if (!HIST && a.ws2_xrange) {   // A/B: bi = the block's group-relative index, its XCD range
-    long long st, len;
-    int nx, j;
-    hist_xcd_range(bi, nb, ntot, &st, &len, &nx, &j);
-    walk_b = (int)(st + j);
-    walk_n = nx;
-    ntile = j < len ? (int)((len - j + nx - 1) / nx) : 0;
-  }
+  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
   uint32_t* hist = (uint32_t*)(part + 2 * (NTS - 1) * NCG * PART);  // HIST: [2 parities][256][HIST_R]
   uint32_t* codes = hist + 2 * 256 * HIST_R;                         // HIST: [2][NCG][MT][64]
   // HIST, ts = 1 waves: the plane (group-local) being counted, its code-0 count in this lane,
@@ -1835,10 +1290,10 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   int boff[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
-  // tiles walked in order by each call sequence (DMA issue, epilogue, FUSE1 RGB loads)
-  TileWalk w_issue, w_ep, w_rgb;
-  w_issue.init(walk_b, walk_n, a.tiles_y, a.tiles_x);
-  w_ep = w_rgb = w_issue;
+  // tiles walked in order by each call sequence (DMA issue, epilogue)
+  TileWalk w_issue, w_ep;
+  w_issue.init(bi, nb, a.tiles_y, a.tiles_x);
+  w_ep = w_issue;
   if constexpr (HIST)
     for (int q = threadIdx.x; q < 2 * 256 * HIST_R; q += 64 * NW) hist[q] = 0;  // published by the first barrier
   auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
@@ -1885,65 +1340,12 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
     }
   };
 
-  // ---- FUSE1 state: conv1 A fragments / bias / scale, this lane's im2col tap offsets in the
-  // patch (-1: pad tap >= 25), and the RGB bytes of the next patch (ts = 1 waves) ----
-  f16x8 A1[2][2];
-  f32x4 b1[2];
-  int toff[4];  // patch offsets of this lane's 4 tap pairs (k = 2 * pair + e: pair = kh * 3 + kw / 2)
-  float scale1 = 1.f;
-  constexpr int NRGB = (C12_PH * C12_PH + 255) / 256;  // patch pixels per ts = 1 thread
-  uint32_t rgb_b[NRGB][2];  // raw bytes of this thread's patch pixels (ts = 1 waves): r | g << 8, b
-  uint32_t rgb_in = 0;      // bit j: pixel j lies inside the image
-  const int tid1 = (int)threadIdx.x - 256;
-  int pl_type = 0;  // colour plane (0 Y, 1 Cb, 2 Cr) of the patch in rgb_b
-  // plain loads, unpacked only by the next tile's patch phase (no wait before the MFMAs)
-  auto rgb_load = [&](int) {  // called for i = 0, 1, 2, ... in order
-    int p, t0y, t0x;
-    tile_take(w_rgb, p, t0y, t0x);
-    const int n = p % a.nimg;
-    pl_type = p / a.nimg;
-    const int py0 = 2 * (2 * t0y - a.pad_y) - a.p1y, px0 = 2 * (2 * t0x - a.pad_x) - a.p1x;
-    const uint8_t* img = a.rgb + (size_t)n * a.H0 * a.W0 * 3;
-    rgb_in = 0;
-#pragma unroll
-    for (int j = 0; j < NRGB; ++j) {
-      const int idx = tid1 + 256 * j;
-      const int r = idx / C12_PH, c = idx - r * C12_PH;
-      const int gy = py0 + r, gx = px0 + c;
-      const bool inside = idx < C12_PH * C12_PH && (unsigned)gy < (unsigned)a.H0 && (unsigned)gx < (unsigned)a.W0;
-      const int cy = min(max(gy, 0), a.H0 - 1), cx = min(max(gx, 0), a.W0 - 1);
-      const uint8_t* px = img + ((size_t)cy * a.W0 + cx) * 3;
-      rgb_b[j][0] = *(const uint16_t*)px;  // r, g (unaligned 2-B load)
-      rgb_b[j][1] = px[2];
-      rgb_in |= (inside ? 1u : 0u) << j;
-    }
-  };
-  if constexpr (FUSE1) {
-    const f16x8* wa = (const f16x8*)a.wx1 + (size_t)model * 2 * 2 * 64 + lane;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) A1[ct][hl] = wa[(ct * 2 + hl) * 64];
-      b1[ct] = *(const f32x4*)(a.bias1 + model * 32 + 16 * ct + 4 * g);
-    }
-    scale1 = a.wscale1[model];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pr = 4 * g + j;
-      toff[j] = pr < 15 ? (pr / 3) * C12_PP + 2 * (pr % 3) : -1;
-    }
-    for (int q = threadIdx.x; q < 256; q += 64 * NW) lut[q] = c_u8_to_unit[q];
-    for (int q = threadIdx.x; q < C12_PH * C12_PP; q += 64 * NW) plane[q] = 0.f;  // pad columns
-    if constexpr (TS == 1)
-      if (ntile > 0) rgb_load(0);
-  }
 
   f32x4 acc[MT];
   const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
   int ep_p = 0, ep_y = 0, ep_x = 0;
-  float rmax = 0.f;  // range guard of the split outputs (conv2's, and conv1's into the halo)
-  if constexpr (!FUSE1)
-    if (ntile > 0) issue(0);
+  float rmax = 0.f;  // range guard of the split outputs
+  if (ntile > 0) issue(0);
 #ifdef NIC_STAMPS
   unsigned long long sx[8] = {}, sa, sb;
   NIC_PNOW(sa);
@@ -2005,9 +1407,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       }
     }
     if (i == ntile) break;
-    if constexpr (!FUSE1) {
-      if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
-    }
+    if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
     if constexpr (HIST) {
       h2_p = h1_p;
       h2_y = h1_y;
@@ -2017,94 +1417,7 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       h1_x = ep_x;
     }
     tile_take(w_ep, ep_p, ep_y, ep_x);
-    const char* buf = lds + (FUSE1 ? 0 : (i & 1)) * G::HALO_BYTES;
-    if constexpr (FUSE1) {
-      // colour plane of the patch (utils.py:74-77: x/255, ((r k0 + g k1) + b k2) + off, every op
-      // rounded), zero outside the image (conv1's SAME padding)
-      if constexpr (TS == 1) {
-        const float* kk = c_ycbcr + pl_type * 3;
-        const float off = c_ycbcr_off[pl_type];
-#pragma unroll
-        for (int j = 0; j < NRGB; ++j) {
-          const int idx = tid1 + 256 * j;
-          if (idx < C12_PH * C12_PH) {
-            const int r = idx / C12_PH, c = idx - r * C12_PH;
-            plane[r * C12_PP + c] = ((rgb_in >> j) & 1)
-                                        ? __fadd_rn(project(kk, lut[rgb_b[j][0] & 255], lut[rgb_b[j][0] >> 8], lut[rgb_b[j][1]]), off)
-                                        : 0.f;
-          }
-        }
-      }
-      WS2_MARK(1);  // epilogue (ts 0) / patch (ts 1)
-      lds_reads_done();
-      stage_barrier();  // patch complete
-      WS2_MARK(2);
-      // conv1 on the 19 x 19 halo pixels: px-tiles of 16, two 16-channel tiles each
-      char* halo = lds;
-      const int c1y0 = 2 * ep_y - a.pad_y, c1x0 = 2 * ep_x - a.pad_x;  // halo origin, conv1-output coords
-      // three px-tiles per wave, software-pipelined: all patch reads, then the splits, then
-      // six independent MFMA chains, then the epilogues
-      constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + NW - 1) / NW;
-      f32x2 xv[PTW][4];
-#pragma unroll
-      for (int u = 0; u < PTW; ++u) {
-        const int q = 16 * (wave + NW * u) + l16;
-        const int qq = q < G::HH * G::HW ? q : 0;
-        const int hy = qq / G::HW, hx = qq - hy * G::HW;
-        const float* pb = plane + 2 * hy * C12_PP + 2 * hx;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xv[u][j] = toff[j] >= 0 ? *(const f32x2*)(pb + toff[j]) : (f32x2){0.f, 0.f};
-      }
-      f16x8 bh[PTW], bl[PTW];
-#pragma unroll
-      for (int u = 0; u < PTW; ++u)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = xv[u][j >> 1][j & 1];
-          const _Float16 hh = (_Float16)x;
-          bh[u][j] = hh;
-          bl[u][j] = (_Float16)(x - (float)hh);
-        }
-      f32x4 c1[PTW][2];
-#pragma unroll
-      for (int u = 0; u < PTW; ++u)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][1], bh[u], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bl[u], c1[u][ct], 0, 0, 0);
-          c1[u][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[ct][0], bh[u], c1[u][ct], 0, 0, 0);
-        }
-#pragma unroll
-      for (int u = 0; u < PTW; ++u) {
-        const int pt = wave + NW * u;
-        if (pt >= NPT) break;  // wave-uniform
-        const int q = 16 * pt + l16;
-        const bool qv = q < G::HH * G::HW;
-        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
-        const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          f32x4 v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = in1 ? leaky02(scale_bias(c1[u][ct][r], scale1, b1[ct][r])) : 0.f;
-          range_track(rmax, v);
-          f16x4 hi, lo;
-          split4(v, hi, lo);
-          if (qv) {
-            char* d = halo + hy * G::RPB + G::col(hx) * G::PSB + (16 * ct + 4 * g) * 2;
-            *(f16x4*)d = hi;
-            *(f16x4*)(d + CIN * 2) = lo;
-          }
-        }
-      }
-      WS2_MARK(3);  // conv1
-      if constexpr (TS == 1)
-        if (i + 1 < ntile) rgb_load(i + 1);  // in flight during this tile's conv2 MFMAs
-      WS2_MARK(4);
-      lds_reads_done();
-      stage_barrier();  // halo complete
-      WS2_MARK(5);
-    }
+    const char* buf = lds + (i & 1) * G::HALO_BYTES;
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // NT taps x KST k32-steps x MT pixel tiles, B fragments read DEPTH groups ahead
@@ -2185,8 +1498,9 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 }
 
 // conv1 + conv2 fused and software-pipelined (split-f16; encoder.py:10-11, 20-21 with the
-// colour front end utils.py:74-77), the tap-split weight-stationary form of ws2_wave with
-// two conv2 halo buffers so that conv1 of tile i+1 runs beside conv2 of tile i.
+// colour front end utils.py:74-77): conv2 weight-stationary on 8 x 8 output tiles, conv1
+// computed per tile into conv2's LDS halo (its 19 x 19 outputs), two halo buffers so that conv1
+// of tile i+1 runs beside conv2 of tile i (c12r_wave below).
 //
 // The colour planes come from a pre-pass (colour_split_kernel): every RGB pixel's Y, Cb, Cr
 // (x/255, ((r k0 + g k1) + b k2) + off, every op rounded) split once into f16 hi / lo
@@ -2196,27 +1510,44 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
 // (Computing the patch per tile from the RGB bytes -- each colour value 6.6 times over,
 // plus the split per im2col element -- made the kernel VALU-issue bound.)
 //
-// One block barrier per tile.  After B_top(i): halo i, patch i+1 and the partials of
-// tile i-1 are complete.
-//   ts 0: epilogue(i-1) (own sums + the ts 1 partials) -> flag -> its conv1(i+1) share ->
-//         conv2 stream of tile i
-//   ts 1: patch DMA of tile i+2 -> conv2 stream of tile i -> (flag: partials(i-1) read) ->
-//         partials(i) -> its conv1(i+1) share -> vmcnt(0)
-// The partials pass only between the two waves of one channel group (SIMD partners w and
-// w + 4), so an LDS flag orders them instead of a second block barrier.  conv1 of tile k
-// writes halo buffer k & 1 and reads patch buffer k & 1.
-// LDS: 2 halos (2 x 57 KB) + partials 16 KB + 2 patches (2 x 7 KB).
-constexpr int C12_PPW = 21;                          // patch row pitch in dwords (42 f16 columns)
-constexpr int C12_PPIECE = (C12_PH * C12_PPW + 63) / 64;  // 1-dword-per-lane DMA pieces per plane (14)
-constexpr int C12_PLANE = C12_PPIECE * 64 * 4;       // bytes per patch plane in LDS (hi or lo)
-#ifndef NIC_C12_PT0
-#define NIC_C12_PT0 3  // conv1 pixel tiles of each ts 0 wave (the ts 1 waves take the rest; 2-6 measured)
-#endif
-#ifndef NIC_C12_PRIO
-// ts 0's conv2 stream at priority 2 over ts 1's: conv12 0.2433-0.2441 vs 0.2446-0.2459 ms (3
-// alternating rounds, profiles/r4_ab_logs.txt); 0 (A/B build): both at priority 1
-#define NIC_C12_PRIO 1
-#endif
+// patch row pitch in dwords (2 x C12_PPW f16 columns, the first 41 used).  A multiple of 4: rows
+// of whole 16-B chunks, DMA'd 1 KB per piece (10 pieces per tile; pitch 21 took 28 one-dword
+// pieces), and the im2col ds_read_b32 groups meet 746 LDS
+// cycles per tile instead of 866 (tools/c12_lds_banks.py)
+constexpr int C12_PPW = 28;
+constexpr int C12_PDW = C12_PPW % 4 == 0 ? 4 : 1;  // dwords per lane of one DMA piece
+constexpr int C12_PPIECE = (C12_PH * C12_PPW + 64 * C12_PDW - 1) / (64 * C12_PDW);  // DMA pieces per plane
+constexpr int C12_PLANE = C12_PPIECE * 64 * 4 * C12_PDW;  // bytes per patch plane in LDS (hi or lo)
+constexpr int C12_NPD = (2 * C12_PPIECE + 3) / 4;         // pieces per issuing wave (4 waves)
+
+// The colour-patch DMA of conv12 (tile -> patch buffer), issued by 4 waves (index cg): piece
+// k = cg + 4 j of the tile's 2 x C12_PPIECE pieces.  Per lane and piece the byte offset from the
+// patch origin in a colour plane, resolved once.
+struct C12PatchDma {
+  unsigned doff[C12_NPD];
+  __device__ __forceinline__ void init(int cg, int lane, int cp_w) {
+#pragma unroll
+    for (int j = 0; j < C12_NPD; ++j) {
+      const int k = cg + 4 * j, q = (k % C12_PPIECE) * 64 * C12_PDW + lane * C12_PDW;  // dword in the plane
+      const int row = q / C12_PPW, dc = q - row * C12_PPW;
+      doff[j] = k < 2 * C12_PPIECE && q < C12_PH * C12_PPW ? (unsigned)((row * cp_w + 2 * dc) * 2) : kDmaOOR;
+    }
+  }
+  __device__ __forceinline__ void issue(const ConvArgs& a, int cg, int p, int t0y, int t0x, char* dst) const {
+    const size_t cp_plane = (size_t)a.cp_h * a.cp_w;  // f16 elements per colour plane
+    const unsigned org = (unsigned)((4 * t0y * a.cp_w + 4 * t0x) * 2);
+#pragma unroll
+    for (int j = 0; j < C12_NPD; ++j) {
+      const int k = cg + 4 * j;  // wave-uniform
+      if (k >= 2 * C12_PPIECE) break;
+      const int hl = k / C12_PPIECE;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.cplane + ((size_t)hl * a.P + p) * cp_plane), (short)0, (int)(cp_plane * 2), kBufWord3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + hl * C12_PLANE + (k % C12_PPIECE) * 256 * C12_PDW),
+                                               4 * C12_PDW, (int)(doff[j] == kDmaOOR ? kDmaOOR : doff[j] + org), 0, 0, 0);
+    }
+  }
+};
 
 // Padded colour planes of the fused conv1 (ConvArgs::cplane): origin offsets and sizes in
 // f16 elements for conv2's tile grid, so that tile (ty, tx)'s patch starts at row 32 ty,
@@ -2299,124 +1630,177 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
   }
 }
 
-template <int TS>
-__device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
-  constexpr int CIN = 32, COUT = 64, NTS = 2, TH = 8, TW = 8, MT = 4, NCG = 4, KST = 1;
-  constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
-  using G = GeomS2<CIN, TH, TW>;
-  constexpr int TAP_BYTES = CIN * COUT * 4;
-  constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
-  char* part = lds + 2 * G::HALO_BYTES;           // [NCG] partial tiles of the ts = 1 waves
-  char* patches = part + NCG * PART;              // [2 parities][hi, lo] patch planes
-  int* pflag = (int*)(patches + 4 * C12_PLANE);   // [NCG] last tile whose partials ts 0 has read
 
+// conv1 + conv2 with specialised roles: each SIMD holds one conv2 wave (R2: all 25
+// taps of 16 output channels resident, 200 VGPRs of w_hi / w_lo; a bare MFMA stream per tile)
+// and one "vector" wave (R1: the conv2 epilogue of those 16 channels, a quarter of conv1, the
+// colour-patch DMA).  In the tap-split form both waves of a SIMD carry a stream and vector
+// work, and the ts 0 wave's chain (epilogue, conv1 share, stream) sets the tile period while
+// its conv1 MFMAs wait behind the partner's stream; here the vector wave's MFMAs (conv1) run
+// at priority over the bare stream, whose only other work is 4 accumulator stores per tile.
+// One block barrier per tile.  After B_top(i): halo i (conv1(i), written in period i-1) and
+// patch i+1 are complete, and acc(i-1) (stored by R2 before B_top(i)) is in LDS.
+//   R2: stream(i) on halo i&1 -> (flag: acc(i-1) read) -> acc(i) to LDS
+//   R1: acc(i-1) from LDS -> flag -> patch DMA(i+2) -> epilogue(i-1) -> conv1(i+1) into halo
+//       (i+1)&1 -> vmcnt: patch(i+2) landed
+// The accumulator tile passes between the two waves of a SIMD only (one per channel group),
+// so the LDS flag orders its reuse.  Different summation order from the tap-split form (one
+// 75-MFMA chain per output instead of two 36 / 39 chains added in fp32): a different fp32
+// rounding of the same sums, within the oracle contract.
+template <int ROLE>
+__device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
+  constexpr int CIN = 32, COUT = 64, MT = 4, NCG = 4;
+  using G = GeomS2<CIN, 8, 8>;
+  constexpr int TAP_BYTES = CIN * COUT * 4;
+  constexpr int PART = MT * 1024;                 // one accumulator tile: MT x 64 lanes x 16 B
+  char* accs = lds + 2 * G::HALO_BYTES;           // [NCG] accumulator tiles
+  char* patches = accs + NCG * PART;              // [2 parities][hi, lo] patch planes
+  int* pflag = (int*)(patches + 4 * C12_PLANE);   // [NCG] last tile whose acc R1 has read
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int cg = wave % NCG;
+  const int cg = wave & 3;
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   const int per_plane = a.tiles_y * a.tiles_x;
   const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
   const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  float rmax = 0.f;
+  if (threadIdx.x < NCG) pflag[threadIdx.x] = 0;
+#ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
+  unsigned long long sx[8] = {}, sa, sb;
+  const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
+  NIC_PNOW(sa);
+#define C12R_MARK(kk)  \
+  do {                 \
+    NIC_PNOW(sb);      \
+    sx[kk] += sb - sa; \
+    sa = sb;           \
+  } while (0)
+#else
+#define C12R_MARK(kk) \
+  do {                \
+  } while (0)
+#endif
 
-  f16x8 wr[NT][KST][2];
-  {
-    const char* wsrc = (const char*)a.wx + ((size_t)model * 25 + T0) * TAP_BYTES;
+  if constexpr (ROLE == 2) {
+    f16x8 wr[25][2];
+    {
+      const char* wsrc = (const char*)a.wx + (size_t)model * 25 * TAP_BYTES;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KST; ++ks)
+      for (int t = 0; t < 25; ++t)
 #pragma unroll
         for (int hl = 0; hl < 2; ++hl)
-          wr[t][ks][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
-                                          ((((2 * ks + (g >> 1)) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
-  }
-  const float scale = a.wscale[model];
-  const int co0 = cg * 16 + 4 * g;
-  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
-  int boff[MT];  // B fragment of pixel tile m at tap (0, 0): halo row 2 (2m + l16/8), column l16 % 8
-#pragma unroll
-  for (int m = 0; m < MT; ++m) boff[m] = 2 * (2 * m + (l16 >> 3)) * G::RPB + (l16 & 7) * G::PSB + g * 16;
-  // tiles walked in order by each call sequence (patch DMA, conv1, epilogue)
-  TileWalk w_patch, w_c1, w_ep;
-  w_patch.init(bi, nb, a.tiles_y, a.tiles_x);
-  w_c1 = w_ep = w_patch;
-  auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
-    int pl, ty, tx;
-    w.take(pl, ty, tx);
-    p = p0 + pl;
-    t0y = ty * TH;
-    t0x = tx * TW;
-  };
-
-
-  // conv1 A fragments / bias / scale and this lane's im2col tap-pair offsets in a patch
-  // plane (bytes; pair = kh * 3 + kw / 2; pad pairs >= 15 read any finite element: their
-  // weights are zero)
-  f16x8 A1[2][2];
-  f32x4 b1[2];
-  {
-    const f16x8* wa = (const f16x8*)a.wx1 + (size_t)model * 2 * 2 * 64 + lane;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) A1[ct][hl] = wa[(ct * 2 + hl) * 64];
-      b1[ct] = *(const f32x4*)(a.bias1 + model * 32 + 16 * ct + 4 * g);
+          wr[t][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES + ((((g >> 1) * 2 + hl) * 2 + (g & 1)) * COUT + cg * 16 + l16) * 16);
     }
-  }
-  const float scale1 = a.wscale1[model];
-  int poff[4];
+    // B fragment of pixel tile m at tap (0, 0): halo row 2 (2m + l16/8), column l16 % 8
+    const int boff = 2 * (l16 >> 3) * G::RPB + (l16 & 7) * G::PSB + g * 16;
+    lds_reads_done();
+    stage_barrier();  // prologue barrier 1 (patches 0, 1)
+    stage_barrier();  // prologue barrier 2 (halo 0)
+    C12R_MARK(6);
+    for (int i = 0; i < ntile; ++i) {
+      const char* buf = lds + (i & 1) * G::HALO_BYTES + boff;
+      f32x4 acc[MT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int pr = 4 * g + j;
-    poff[j] = pr < 15 ? ((pr / 3) * C12_PPW + pr % 3) * 4 : 0;
-  }
-  // ts 1: the patch DMA of a tile, 2 planes x C12_PPIECE pieces over the 4 ts 1 waves;
-  // per lane and piece the byte offset from the patch origin in a colour plane
-  constexpr int NPD = (2 * C12_PPIECE + 3) / 4;  // pieces per ts 1 wave (7)
-  unsigned doff[NPD];
-  if constexpr (TS == 1) {
+      for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      constexpr int NG = 25 * MT, DEPTH = 2;  // B-fragment groups read ahead (3: no faster)
+      auto grp_off = [](int gq) {
+        const int t = gq / MT, m = gq - t * MT, kh = t / 5, kw = t - kh * 5;
+        return 4 * m * G::RPB + kh * G::RPB + G::col(kw) * G::PSB;
+      };
+      f16x8 fb[DEPTH][2];
 #pragma unroll
-    for (int j = 0; j < NPD; ++j) {
-      const int k = cg + 4 * j, q = (k % C12_PPIECE) * 64 + lane;
-      const int row = q / C12_PPW, dc = q - row * C12_PPW;
-      doff[j] = k < 2 * C12_PPIECE && q < C12_PH * C12_PPW ? (unsigned)((row * a.cp_w + 2 * dc) * 2) : kDmaOOR;
+      for (int gq = 0; gq < DEPTH; ++gq) {
+        fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
+        fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
+      }
+#if defined(NIC_DIAG_C12R) && NIC_DIAG_C12R == 2  // diagnostic: no R2 stream at all (R1 alone)
+      if (false)
+#endif
+      static_for<NG>([&](auto gqc) {
+        constexpr int gq = decltype(gqc)::value;
+        constexpr int t = gq / MT, m = gq - t * MT;
+        f16x8(&cur)[2] = fb[gq % DEPTH];
+#if defined(NIC_DIAG_C12R) && NIC_DIAG_C12R == 1  // diagnostic: the stream's LDS reads, no MFMAs
+        asm volatile("" ::"v"(cur[0]), "v"(cur[1]), "v"(wr[t][0]), "v"(wr[t][1]));
+#else
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][1], cur[0], acc[m], 0, 0, 0);  // w_lo*a_hi
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][0], cur[1], acc[m], 0, 0, 0);  // w_hi*a_lo
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][0], cur[0], acc[m], 0, 0, 0);  // w_hi*a_hi
+#endif
+        if constexpr (gq + DEPTH < NG) {
+          cur[0] = *(const f16x8*)(buf + grp_off(gq + DEPTH));
+          cur[1] = *(const f16x8*)(buf + grp_off(gq + DEPTH) + CIN * 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the stream order
+      });
+      C12R_MARK(5);
+      if (i > 0)
+        while (__hip_atomic_load(pflag + cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < i)
+          __builtin_amdgcn_s_sleep(1);
+      char* pp = accs + cg * PART + lane * 16;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+      lds_reads_done();  // (lgkmcnt 0: the acc stores too) before the barrier publishes them
+      C12R_MARK(2);
+      stage_barrier();   // B_top(i+1)
+      C12R_MARK(0);
     }
-  }
-  const size_t cp_plane = (size_t)a.cp_h * a.cp_w;  // f16 elements per colour plane
-  auto patch_dma = [&](int i) {  // tile i's patch into patch buffer i & 1
-    int p, t0y, t0x;
-    tile_take(w_patch, p, t0y, t0x);  // patch_dma is called for i = 0, 1, 2, ... in order
-    const unsigned org = (unsigned)((4 * t0y * a.cp_w + 4 * t0x) * 2);
-    char* dst = patches + (i & 1) * 2 * C12_PLANE;
+  } else {
+    __builtin_amdgcn_s_setprio(1);  // the vector wave's MFMAs and VALU ahead of the bare stream
+    TileWalk w_patch, w_c1, w_ep;
+    w_patch.init(bi, nb, a.tiles_y, a.tiles_x);
+    w_c1 = w_ep = w_patch;
+    auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
+      int pl, ty, tx;
+      w.take(pl, ty, tx);
+      p = p0 + pl;
+      t0y = ty * 8;
+      t0x = tx * 8;
+    };
+    f16x8 A1[2][2];
+    f32x4 b1[2];
+    {
+      const f16x8* wa = (const f16x8*)a.wx1 + (size_t)model * 2 * 2 * 64 + lane;
 #pragma unroll
-    for (int j = 0; j < NPD; ++j) {
-      const int k = cg + 4 * j;  // wave-uniform
-      if (k >= 2 * C12_PPIECE) break;
-      const int hl = k / C12_PPIECE;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.cplane + ((size_t)hl * a.P + p) * cp_plane), (short)0, (int)(cp_plane * 2), kBufWord3);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + hl * C12_PLANE + (k % C12_PPIECE) * 256), 4,
-                                               (int)(doff[j] == kDmaOOR ? kDmaOOR : doff[j] + org), 0, 0, 0);
+      for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) A1[ct][hl] = wa[(ct * 2 + hl) * 64];
+        b1[ct] = *(const f32x4*)(a.bias1 + model * 32 + 16 * ct + 4 * g);
+      }
     }
-  };
-  float rmax = 0.f;  // range guard of the split outputs (conv2's, and conv1's into the halo)
-  // this role's share of conv1 of tile i on the 19 x 19 halo pixels (patch buffer i & 1 ->
-  // halo buffer i & 1): pixel tiles PTB + cg + 4u, two 16-channel tiles each, software-
-  // pipelined (all fragment reads, then the MFMA chains, then the epilogues)
-  auto conv1 = [&](int i) {
-    constexpr int NPT = (G::HH * G::HW + 15) / 16, PT0 = NIC_C12_PT0, PT1 = (NPT - 4 * PT0 + 3) / 4;
-    static_assert(PT0 >= 0 && PT1 >= 0 && 4 * (PT0 + PT1) >= NPT, "conv1 shares cover the halo");
-    constexpr int PTW = TS == 0 ? PT0 : PT1, PTB = TS == 0 ? 0 : 4 * PT0;
-    if constexpr (PTW > 0) {
+    const float scale1 = a.wscale1[model];
+    const float scale = a.wscale[model];
+    const int co0 = cg * 16 + 4 * g;
+    const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + co0);
+    int poff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pr = 4 * g + j;
+      poff[j] = pr < 15 ? ((pr / 3) * C12_PPW + pr % 3) * 4 : 0;
+    }
+    // the patch DMA stays with R1: issued by R2 instead (its stream has ~1,000 cycles of slack
+    // per tile) conv12 measured 1 % slower
+    C12PatchDma pdma;
+    pdma.init(cg, lane, a.cp_w);
+    auto patch_dma = [&](int i) {  // tile i's patch into patch buffer i & 1 (called in order)
       int p, t0y, t0x;
-      tile_take(w_c1, p, t0y, t0x);  // conv1 is called for i = 0, 1, 2, ... in order
+      tile_take(w_patch, p, t0y, t0x);
+      pdma.issue(a, cg, p, t0y, t0x, patches + (i & 1) * 2 * C12_PLANE);
+    };
+    // conv1 of tile i on this wave's pixel tiles cg + 4u of the 19 x 19 halo (patch buffer
+    // i & 1 -> halo buffer i & 1), software-pipelined: all fragment reads, then the MFMA chains,
+    // then the epilogues
+    auto conv1 = [&](int i) {
+      constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + 3) / 4;
+      int p, t0y, t0x;
+      tile_take(w_c1, p, t0y, t0x);
       char* halo = lds + (i & 1) * G::HALO_BYTES;
       const char* ph = patches + (i & 1) * 2 * C12_PLANE;
-      const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;  // halo origin, conv1-output coords
+      const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;
       f16x8 bh[PTW], bl[PTW];
 #pragma unroll
       for (int u = 0; u < PTW; ++u) {
-        const int q = 16 * (PTB + cg + 4 * u) + l16;
+        const int q = 16 * (cg + 4 * u) + l16;
         const int qq = q < G::HH * G::HW ? q : 0;
         const int hy = qq / G::HW, hx = qq - hy * G::HW;
         const char* pb = ph + (2 * hy * C12_PPW + hx) * 4;
@@ -2440,7 +1824,7 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
         }
 #pragma unroll
       for (int u = 0; u < PTW; ++u) {
-        const int pt = PTB + cg + 4 * u;
+        const int pt = cg + 4 * u;
         if (pt >= NPT) break;  // wave-uniform
         const int q = 16 * pt + l16;
         const bool qv = q < G::HH * G::HW;
@@ -2454,148 +1838,61 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
           range_track(rmax, v);
           f16x4 hi, lo;
           split4(v, hi, lo);
-          // swap16_pair: even-g lanes hold the hi of channels 16 ct + 4 g .. +7, odd-g lanes
-          // the lo of the same 8: one 16-B store per lane (2-way bank conflicts with the
-          // 160-B records) instead of two 8-B stores (4-way)
           const u32x4 q16 = swap16_pair(hi, lo);
           if (qv)
             *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * ct + 4 * (g & ~1)) * 2) = q16;
         }
       }
-    }
-  };
-  f32x4 acc[MT];
-  // conv2 of tile i: this wave's NT taps x MT pixel tiles on halo buffer i & 1, B fragments
-  // DEPTH groups ahead
-  auto stream = [&](int i) {
-    const char* buf = lds + (i & 1) * G::HALO_BYTES;
-#pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    constexpr int NG = NT * KST * MT, DEPTH = 3;
-    auto grp_off = [&](int gq) {
-      const int st = gq / MT, m = gq - st * MT;
-      const int t = T0 + st / KST, kh = t / 5, kw = t - kh * 5;
-      return boff[m] + kh * G::RPB + G::col(kw) * G::PSB;
     };
-    f16x8 fb[DEPTH][2];
-#pragma unroll
-    for (int gq = 0; gq < DEPTH; ++gq) {
-      fb[gq][0] = *(const f16x8*)(buf + grp_off(gq));
-      fb[gq][1] = *(const f16x8*)(buf + grp_off(gq) + CIN * 2);
-    }
-    // NIC_C12_PRIO: the ts 0 wave's conv2 stream (its chain is the tile period by stamps) outranks
-    // the ts 1 partner's when both have an MFMA ready
-    __builtin_amdgcn_s_setprio(NIC_C12_PRIO && TS == 0 ? 2 : 1);
-    static_for<NG>([&](auto gqc) {
-      constexpr int gq = decltype(gqc)::value;
-      constexpr int st = gq / MT, m = gq - st * MT, t = st / KST, ks = st % KST;
-      f16x8(&cur)[2] = fb[gq % DEPTH];
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], cur[0], acc[m], 0, 0, 0);  // w_lo*a_hi
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[1], acc[m], 0, 0, 0);  // w_hi*a_lo
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], cur[0], acc[m], 0, 0, 0);  // w_hi*a_hi
-      if constexpr (gq + DEPTH < NG) {
-        cur[0] = *(const f16x8*)(buf + grp_off(gq + DEPTH));
-        cur[1] = *(const f16x8*)(buf + grp_off(gq + DEPTH) + CIN * 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the stream order
-    });
-    __builtin_amdgcn_s_setprio(NIC_C12_PRIO == 2 && TS == 0 ? 2 : 0);
-  };
-  const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
-  // epilogue of tile i (called for i = 0, 1, 2, ... in order by the ts 0 waves): its own sums +
-  // the ts 1 partials
-  auto epilogue = [&](int i) {
-    int p, t0y, t0x;
-    tile_take(w_ep, p, t0y, t0x);
-    const char* pp = part + cg * PART + lane * 16;
-    f32x4 q4[MT];  // all partial reads in flight before the first use
-#pragma unroll
-    for (int m = 0; m < MT; ++m) q4[m] = *(const f32x4*)(pp + m * 1024);
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const f32x4 q = q4[m];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[m][r] = __fadd_rn(acc[m][r], q[r]);
-      const int oy = t0y + 2 * m + (l16 >> 3), ox = t0x + (l16 & 7);
-      f32x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
-      const bool inside = oy < a.OH && ox < a.OW;
-      if (inside) range_track(rmax, v);
-      f16x4 hi, lo;
-      split4(v, hi, lo);
-      const u32x4 qv = swap16_pair(hi, lo);
-      if (inside) *(u32x4*)(a.out_s + (((size_t)p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = qv;
-    }
-  };
-
-  // prologue: patches 0 and 1, conv1 of tile 0
-  if (threadIdx.x < NCG) pflag[threadIdx.x] = 0;
-  if constexpr (TS == 1) {
+    const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
+    // prologue: patches 0, 1 -> barrier -> conv1(0) -> barrier
     if (ntile > 0) patch_dma(0);
     if (ntile > 1) patch_dma(1);
     dma_wait_all();
-  }
-  lds_reads_done();
-  stage_barrier();  // patches 0, 1 complete
-  if (ntile > 0) conv1(0);
-  if constexpr (NIC_C12_PRIO == 2 && TS == 0) __builtin_amdgcn_s_setprio(2);  // A/B: ts 0's whole chain first
-#ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
-  unsigned long long sx[8] = {}, sa, sb;
-  const unsigned long long s_rt0 = __builtin_amdgcn_s_memrealtime(), s_c0 = __builtin_amdgcn_s_memtime();
-  NIC_PNOW(sa);
-#define C12_MARK(kk)   \
-  do {                 \
-    NIC_PNOW(sb);      \
-    sx[kk] += sb - sa; \
-    sa = sb;           \
-  } while (0)
-#else
-#define C12_MARK(kk) \
-  do {               \
-  } while (0)
-#endif
-  // One block barrier per tile.  After B_top(i): halo i, patch i+1 and the partials of
-  // tile i-1 are complete.
-  //   ts 0: epilogue(i-1) (reads the partials) -> flag -> its conv1(i+1) share -> stream(i)
-  //   ts 1: RGB loads of tile i+2 -> stream(i) -> (flag: partials(i-1) read) -> partials(i)
-  //         -> its conv1(i+1) share -> patch(i+2) into the buffer conv1(i) read
-  // The partials pass between the two waves of one channel group only (SIMD partners), so
-  // an LDS flag orders them instead of a second block barrier.
-  for (int i = 0; i <= ntile; ++i) {
-    C12_MARK(6);
+    stage_barrier();
+    if (ntile > 0) conv1(0);
     lds_reads_done();
-    stage_barrier();  // B_top
-    C12_MARK(0);
-    if constexpr (TS == 0) {
+    stage_barrier();
+    C12R_MARK(6);
+    for (int i = 0; i <= ntile; ++i) {
       if (i > 0) {
-        epilogue(i - 1);
-        lds_reads_done();  // the partial reads have returned
-        __hip_atomic_store(pflag + cg, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      C12_MARK(1);
-      if (i == ntile) break;
-      if (i + 1 < ntile) conv1(i + 1);
-      C12_MARK(3);
-      stream(i);
-      C12_MARK(5);
-    } else {
-      if (i == ntile) break;
-      if (i + 2 < ntile) patch_dma(i + 2);  // into the buffer conv1(i) read; lands during the stream
-      C12_MARK(4);
-      stream(i);
-      C12_MARK(5);
-      if (i > 0)
-        while (__hip_atomic_load(pflag + cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < i)
-          __builtin_amdgcn_s_sleep(1);
-      C12_MARK(2);
-      char* pp = part + cg * PART + lane * 16;
+        // acc(i-1) of this channel group, then the flag that frees the buffer for R2
+        const char* pp = accs + cg * PART + lane * 16;
+        f32x4 acc[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
+        for (int m = 0; m < MT; ++m) acc[m] = *(const f32x4*)(pp + m * 1024);
+        lds_reads_done();
+        __hip_atomic_store(pflag + cg, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (i + 2 < ntile) patch_dma(i + 2);  // into buffer i&1, which conv1(i) read in period i-1
+        int p, t0y, t0x;
+        tile_take(w_ep, p, t0y, t0x);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int oy = t0y + 2 * m + (l16 >> 3), ox = t0x + (l16 & 7);
+          f32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
+          const bool inside = oy < a.OH && ox < a.OW;
+          if (inside) range_track(rmax, v);
+          f16x4 hi, lo;
+          split4(v, hi, lo);
+          const u32x4 qv = swap16_pair(hi, lo);
+          if (inside) *(u32x4*)(a.out_s + (((size_t)p * a.OH + oy) * a.OW + ox) * COUT * 2 + st_off) = qv;
+        }
+      }
+      C12R_MARK(1);
+      if (i == ntile) break;
+      if (i == 0 && ntile > 2) patch_dma(2);
+#if defined(NIC_DIAG_C12R) && NIC_DIAG_C12R == 3  // diagnostic: no conv1 (R2 alone, stale halos)
+      if (false)
+#endif
       if (i + 1 < ntile) conv1(i + 1);
-      C12_MARK(3);
-      dma_wait_all();  // patch i+2 landed (before B_top(i+1) publishes it)
-      C12_MARK(1);
+      C12R_MARK(3);
+      dma_wait_all();   // patch(i+2) landed (the epilogue's stores too)
+      lds_reads_done();
+      C12R_MARK(4);
+      stage_barrier();  // B_top(i+1)
+      C12R_MARK(0);
     }
   }
 #ifdef NIC_STAMPS
@@ -2604,17 +1901,17 @@ __device__ __forceinline__ void c12_wave(const ConvArgs& a, char* lds, int model
 #pragma unroll
     for (int q = 0; q < 7; ++q) o[q] = sx[q];
     o[7] = ntile;
-    if (wave == 0) {  // shader clock: cycles and 100 MHz ticks of the loop, after the stamp area
+    if (wave == 0) {
       g_stamps[256 * 64 + 2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - s_c0;
       g_stamps[256 * 64 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - s_rt0;
     }
   }
 #endif
-#undef C12_MARK
+#undef C12R_MARK
   range_report(a.rg, rmax);
 }
 
-// XCD-contiguous tile positions (ConvArgs::tile_xcd): block b of a group of nb runs on XCD
+// XCD-contiguous tile positions: block b of a group of nb runs on XCD
 // (base + b) % 8, so give the blocks of one XCD consecutive positions in each round of nb
 // tiles -- neighbouring tiles, whose halos overlap, are then fetched into one L2.
 __device__ __forceinline__ int xcd_pos(int b, int nb) {
@@ -2630,14 +1927,14 @@ __global__ __launch_bounds__(512) void conv12_kernel(ConvArgs a) {
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  const int bi = a.tile_xcd ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
+  const int bi = xcd_pos(blockIdx.x - a.ws_blk[gi], nb);
   if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < 4)
-    c12_wave<0>(a, lds, gi, bi, nb);
+    c12r_wave<2>(a, lds, gi, bi, nb);
   else
-    c12_wave<1>(a, lds, gi, bi, nb);
+    c12r_wave<1>(a, lds, gi, bi, nb);
 }
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1, bool HIST = false>
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool HIST = false>
 __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvArgs a) {
   KT_SCOPE(3);
   using G = GeomS2<CIN, TH, 8>;
@@ -2645,16 +1942,15 @@ __global__ __launch_bounds__(64 * (COUT / 16) * NTS) void conv_ws2_kernel(ConvAr
   static_assert(NCG * NTS == 8, "8 waves per block");
   constexpr int PARTS = 2 * (NTS - 1) * NCG * (TH / 2) * 1024;
   __shared__ __attribute__((aligned(16)))
-  char lds[(FUSE1 ? 1 : 2) * G::HALO_BYTES + PARTS + (FUSE1 ? (C12_PH * C12_PP + 256) * 4 : 0) +
-           (HIST ? HIST_LDS : 0)];
+  char lds[2 * G::HALO_BYTES + PARTS + (HIST ? HIST_LDS : 0)];
   int gi = 0;
   while (gi + 1 < a.ws_ngrp && (int)blockIdx.x >= a.ws_blk[gi + 1]) ++gi;
   const int nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  const int bi = a.tile_xcd && !a.ws2_xrange ? xcd_pos(blockIdx.x - a.ws_blk[gi], nb) : blockIdx.x - a.ws_blk[gi];
+  const int bi = xcd_pos(blockIdx.x - a.ws_blk[gi], nb);
   const int ts = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / NCG;
   static_for<NTS>([&](auto tsc) {
     constexpr int TS = decltype(tsc)::value;
-    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS, FUSE1, HIST>(a, lds, gi, bi, nb);
+    if (ts == TS) ws2_wave<CIN, COUT, NTS, TH, OUT_MODE, TS, HIST>(a, lds, gi, bi, nb);
   });
 }
 
@@ -2699,193 +1995,27 @@ __global__ __launch_bounds__(64 * (COUT / 16), 2) void conv_ws_kernel(ConvArgs a
 
 // ------------------------------------------------------------------------------------
 // dconv1 (Conv2DTranspose 32 -> 64, k5 s2 on the dequantised latent, decoder.py:10,20,40-41)
-// as a persistent weight-stationary kernel on the u8 codes.  The one-tile-per-block form
-// (conv_x3_kernel, NIC_D1=x) re-reads all 25 taps of weights from L2 per block (205 KB x
-// 1,536 blocks) and issues ~9 VALU per MFMA around a latency-bound pipeline (PMC: issue stall
-// 0.60, MFMA busy 0.23).  Here, as in dconv7's all-phase blocks: wave w owns output channels
-// 16w..16w+15 and keeps one sub-pixel phase's taps resident (A operand: w_hi, w_lo of 32
-// input channels per tap = 8 VGPRs), a block walks its share of the model's 8 x 8 coarse
-// tiles once per phase, and the codes (0..255, exact in f16) are the B operand: 2 MFMAs per
-// MAC, 1/255 folded into the epilogue scale (one rounding, as conv_x3_kernel).  Halo: 10 x 10
-// coarse pixels of 32 codes, loaded to registers one tile ahead (during the current tile's
-// MFMA stream) and written to LDS as f16 records of 64 B (4 slots) in rows of 800 B (50 slots):
-// for every tap column, each of ds_read_b128's four lane groups ({0-3,12-15,20-27}, ...; lane
-// (g, l16) reads slot g of pixel (l16 / 8, l16 % 8 + kw)) hits 16 distinct 16-B bank slots
-// (exhaustive search over record / row pitches and chunk swizzles; the first layout, 80-B
-// records in 896-B rows, had 50 % LDS bank-conflict cycles by PMC).
+// as a persistent weight-stationary kernel on the u8 codes (codes 0..255 are exact in f16:
+// they are the B operand, 2 MFMAs per MAC, 1/255 folded into the epilogue scale, one
+// rounding), all four sub-pixel phases per staged tile.  A block of 8 waves (one per CU)
+// stages a tile's codes once and runs all 25 taps on it: wave w < 4 holds phases (1,1) and
+// (0,0) (9 + 4 taps), wave w + 4 phases (0,1) and (1,0) (6 + 6 taps) of output channels
+// 16 (w & 3) .. + 15 -- 13 and 12 taps of resident A fragments (w_hi, w_lo of 32 input
+// channels: 8 VGPRs per tap), so the two SIMD partners carry nearly equal MFMA work on one
+// halo and each phase's epilogue overlaps its partner's MFMAs.  Halo: 10 x 10 coarse pixels
+// of 32 codes, loaded to registers two tiles ahead and written to LDS as f16 records of 64 B
+// (4 slots) in rows of 800 B (50 slots): for every tap column, each of ds_read_b128's four
+// lane groups ({0-3,12-15,20-27}, ...; lane (g, l16) reads slot g of pixel (l16 / 8,
+// l16 % 8 + kw)) hits 16 distinct 16-B bank slots (exhaustive search over record / row
+// pitches and chunk swizzles; 80-B records in 896-B rows had 50 % bank-conflict cycles).
+// Earlier forms, measured slower and removed (DESIGN sections 5, 5b): one tile per block
+// (all 25 taps of weights re-read from L2 per block, latency-bound: PMC issue stall 0.60,
+// MFMA busy 0.23) and a per-phase walk (each tile's codes staged four times, 32-72 MFMAs per
+// wave between two barriers).
 // ------------------------------------------------------------------------------------
 constexpr int D1_PSB = 64;           // LDS bytes per halo pixel: 32 f16 codes, unpadded
 constexpr int D1_RPB = 800;          // halo row pitch (10 pixels + 160 B): 50 slots = 2 mod 16
 constexpr int D1_HB = 10 * D1_RPB;   // one halo buffer
-constexpr int D1_LD = 4;             // code dwords per thread per tile (800 over 256 threads)
-
-template <int KH, int KW>
-__device__ __forceinline__ void d1_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
-                                        int px) {
-  constexpr int COUT = 64, MT = 4, NTAPS = KH * KW, TAP_BYTES = 32 * COUT * 4, PXB = COUT * 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-  const int per_plane = a.tiles_y * a.tiles_x;
-  const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
-  const int ntot = np * per_plane;
-  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
-  if (ntile == 0) return;
-
-  // resident weights of this phase: A fragment (row co = 16w + l16, k = channel 8g + j) is the
-  // f16x3 repack's 16-B chunk (k16-step g/2, half g%2) -- the ws_body formula with one k32-step
-  f16x8 wr[NTAPS][2];
-  {
-    const char* wsrc = (const char*)a.wx + ((size_t)model * 25 + tb) * TAP_BYTES;
-#pragma unroll
-    for (int t = 0; t < NTAPS; ++t)
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl)
-        wr[t][hl] = *(const f16x8*)(wsrc + (size_t)t * TAP_BYTES +
-                                    ((((g >> 1) * 2 + hl) * 2 + (g & 1)) * COUT + wave * 16 + l16) * 16);
-  }
-  // 2^-k undoes the weight pre-scale and carries the dequantiser's 1/255: fma(sum, s, b)
-  const float scale = a.wscale[model] * 0.0039215688593685627f;
-  const f32x4 bias = *(const f32x4*)(a.bias + model * COUT + wave * 16 + 4 * g);
-
-  // code staging: thread q = threadIdx.x + 256 j loads dword q & 7 (codes 4c..4c+3) of halo
-  // pixel q >> 3 (row hy, column hx; origin (t0y - 1, t0x - 1))
-  int st_lds[D1_LD], st_hy[D1_LD], st_hx[D1_LD];
-#pragma unroll
-  for (int j = 0; j < D1_LD; ++j) {
-    const int q = threadIdx.x + 256 * j, pix = q >> 3, c = q & 7;
-    st_hy[j] = q < 800 ? pix / 10 : -1000;  // -1000: no dword (out of every image)
-    st_hx[j] = pix - (pix / 10) * 10;
-    st_lds[j] = (pix / 10) * D1_RPB + st_hx[j] * D1_PSB + c * 8;
-  }
-  // codes of the next tile in registers (loads two tiles ahead, 2 x 4 registers, measured
-  // slower: 0.0705 vs 0.0658 ms)
-  uint32_t cq[D1_LD];
-  TileWalk it_ld, it_ep;
-  it_ld.init(bi, nb, a.tiles_y, a.tiles_x);
-  it_ep = it_ld;
-  auto load_codes = [&] {  // the next tile's codes into cq (zeros outside the image)
-    int pl, ty, tx;
-    it_ld.take(pl, ty, tx);
-    const int p = p0 + pl;
-    const uint8_t* base = a.in_u8 + (size_t)(p % a.nimg) * a.H * a.W * 96 + (p / a.nimg) * 32;
-#pragma unroll
-    for (int j = 0; j < D1_LD; ++j) {
-      const int gy = ty * 8 - 1 + st_hy[j], gx = tx * 8 - 1 + st_hx[j];
-      const bool ok = (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-      cq[j] = ok ? *(const uint32_t*)(base + ((size_t)gy * a.W + gx) * 96 + (threadIdx.x & 7) * 4) : 0u;
-    }
-  };
-  auto write_codes = [&](char* buf) {  // cq -> f16 codes (exact) in LDS
-#pragma unroll
-    for (int j = 0; j < D1_LD; ++j) {
-      if (st_hy[j] < 0) continue;
-      const uint32_t q = cq[j];
-      const f16x4 c = {(_Float16)(float)(q & 255), (_Float16)(float)((q >> 8) & 255),
-                       (_Float16)(float)((q >> 16) & 255), (_Float16)(float)(q >> 24)};
-      *(f16x4*)(buf + st_lds[j]) = c;
-    }
-  };
-
-  // B fragment of pixel tile m (coarse pixels (2m + l16/8, l16%8)) at tap (kh, kw): chunk g
-  int bx[KW];
-#pragma unroll
-  for (int kw = 0; kw < KW; ++kw) bx[kw] = (l16 >> 3) * D1_RPB + ((l16 & 7) + kw) * D1_PSB + g * 16;
-  // output granules (fine pixel (2y + py, 2x + px)) through a per-plane buffer resource
-  const int st_off = (g & 1) * COUT + wave * 16 + 8 * (g >> 1);
-  const unsigned out_plane = (unsigned)((size_t)a.OH * a.OW * PXB);
-  unsigned g_off[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int dy = 2 * m + (l16 >> 3), dx = l16 & 7;
-    g_off[m] = (unsigned)(((2 * dy) * a.OW + 2 * dx) * PXB + st_off * 2);
-  }
-  f32x4 acc[MT];
-  float rmax = 0.f;
-  int ep_p = 0, ep_y = 0, ep_x = 0;
-  load_codes();
-  for (int i = 0; i <= ntile; ++i) {
-    char* buf = lds + (i & 1) * D1_HB;
-    if (i < ntile) write_codes(buf);  // buffer i & 1 was last read by tile i-2's stream
-    lds_reads_done();                 // this wave's code writes have landed
-    stage_barrier();                  // tile i's halo complete; tile i-1's stream done everywhere
-    if (i > 0) {  // epilogue of tile i-1: *2^-k/255, bias, leaky, split, 16-B stores
-      const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.out_s + (size_t)ep_p * out_plane / 2), (short)0, (int)out_plane, kBufWord3);
-      const unsigned out_org = (unsigned)(((2 * ep_y + py) * a.OW + 2 * ep_x + px) * PXB);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
-        f32x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
-        const bool in = y < a.H && x < a.W;
-        if (in) range_track(rmax, v);
-        f16x4 hi, lo;
-        split4(v, hi, lo);
-        const u32x4 q = swap16_pair(hi, lo);
-        __builtin_amdgcn_raw_buffer_store_b128(q, out_rs, in ? out_org + g_off[m] : kDmaOOR, 0, 0);
-      }
-    }
-    if (i == ntile) break;
-    {
-      int pl, ty, tx;
-      it_ep.take(pl, ty, tx);
-      ep_p = p0 + pl;
-      ep_y = ty * 8;
-      ep_x = tx * 8;
-    }
-    if (i + 1 < ntile) load_codes();  // lands during this tile's stream
-#pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const unsigned bb = lds_off(buf);
-    auto frag = [&](int m, int t) {
-      const int kh = t / KW, kw = t - kh * KW;
-      return *(const __attribute__((address_space(3))) f16x8*)(lds_at(bb + bx[kw]) + (2 * m + kh) * D1_RPB);
-    };
-    f16x8 fb[MT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) fb[m] = frag(m, 0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int t = 0; t < NTAPS; ++t) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][1], fb[m], acc[m], 0, 0, 0);  // w_lo*c
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][0], fb[m], acc[m], 0, 0, 0);  // w_hi*c
-        if (t + 1 < NTAPS) fb[m] = frag(m, t + 1);
-        __builtin_amdgcn_sched_barrier(0);  // keep the rolling order
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-  range_report(a.rg, rmax);
-}
-
-// Block groups: group gi = blocks [ws_blk[gi], ws_blk[gi + 1]), model gi (Y, CbCr); every block
-// runs the four sub-pixel phases over its share of the model's tiles (as dconv7's blocks)
-__global__ __launch_bounds__(256, 2) void dconv1_ws_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * D1_HB];
-  const int gi = (int)blockIdx.x >= a.ws_blk[1] ? 1 : 0;
-  const int bi = blockIdx.x - a.ws_blk[gi], nb = a.ws_blk[gi + 1] - a.ws_blk[gi];
-  d1_body<3, 3>(a, lds, gi, bi, nb, 16, 1, 1);
-  d1_body<2, 3>(a, lds, gi, bi, nb, 4, 0, 1);
-  d1_body<3, 2>(a, lds, gi, bi, nb, 10, 1, 0);
-  d1_body<2, 2>(a, lds, gi, bi, nb, 0, 0, 0);
-}
-
-// ------------------------------------------------------------------------------------
-// dconv1 with all four sub-pixel phases per staged tile (round 4; NIC_D1=a, see
-// launch_dconv1_all).  dconv1_ws_kernel walks its tiles once per phase: every tile's 10 x 10
-// halo of codes is loaded and converted to f16 four times (PMC: 96 MB fetched for 6.3 MB of
-// codes) and each pass runs only 32-72 MFMAs per wave between two barriers (VALU : MFMA 5.2,
-// SALU : MFMA 3.1, MFMA busy 0.25).  Here a block of 8 waves (one per CU) stages a tile's
-// codes once and runs all 25 taps on it: wave w < 4 holds phases (1,1) and (0,0) (9 + 4 taps),
-// wave w + 4 phases (0,1) and (1,0) (6 + 6 taps) of output channels 16 (w & 3) .. + 15 -- 13 and
-// 12 taps of resident A fragments (w_hi, w_lo of 32 input channels: 8 VGPRs per tap), so the
-// two SIMD partners carry nearly equal MFMA work on one halo and each phase's epilogue
-// overlaps its partner's MFMAs.  Same MFMA chains and epilogue arithmetic as d1_body: the
-// outputs are bit-identical to dconv1_ws_kernel (GPU test).
-// ------------------------------------------------------------------------------------
 constexpr int D1A_LD = 2;  // code dwords per thread per tile (800 over 512 threads)
 #ifndef NIC_D1A_PF
 #define NIC_D1A_PF 2  // code prefetch distance in tiles (1: A/B build)
@@ -3818,554 +2948,6 @@ __global__ __launch_bounds__(256) void dconv8_gather_kernel(Dconv8Args a) {
   d8_store_rgb(a, n, my, mx, outv);
 }
 
-// ------------------------------------------------------------------------------------
-// dconv8 gather through LDS (NIC_D8G=l; the default is dconv8_gather_kernel above).  The
-// direct gather issues 75 dword loads per thread (3 planes x 25 phase taps), each wave
-// instruction touching 8 row pieces of up to 4 projection tiles: it ran at 4.3 TB/s, bound
-// by memory instructions, not bytes.  Here a block (the same 16 x 16 coarse positions m, one
-// image) first copies, per plane, the projections its outputs read into LDS: the four phase
-// tiles of its own 8 x 8 dconv7 tile (4 x 6,400 contiguous bytes, one 16-B load per lane
-// and 400 B) and the edge row / column / corner of the neighbouring tiles that some phase
-// taps reach (489 values, a compile-time list: a window row iy = 0 reaches the row above
-// for odd phase rows, iy = 2 the row below for even ones, likewise columns), then sums each
-// output's 4..9 projections from LDS in the direct kernel's order (bit-identical results).
-// LDS image per plane: S[ph7][tap][ry][rx], 9 x 9 coarse positions per (phase, tap): rows
-// 8 ty - py7 .. 8 ty + 8 - py7 (the extra row on the side that phase reaches), same for x.
-// The next plane's loads are in flight (registers) while this plane is summed.  Measured
-// same-box no faster than the direct gather (0.074-0.076 vs 0.072-0.075 ms, 4.3-4.5 TB/s
-// both): fewer memory instructions did not move the rate, so the direct kernel is not bound
-// by its instruction count; kept as the tested alternative.
-// ------------------------------------------------------------------------------------
-constexpr int D8G_TB[4] = {0, 4, 10, 16};  // phase-major tap bases (dconv8's phase windows)
-constexpr int D8G_S = 4 * 25 * 81;         // floats of one plane's LDS image
-constexpr int D8G_EDGE_MAX = 512;
-struct D8gEdges {
-  unsigned e[D8G_EDGE_MAX];
-  int n;
-};
-// edge entry: bits 0..12 LDS index, 13..23 source float offset inside the tile block
-// (tap * 64 + ly * 8 + lx), 24..25 phase, 26..27 tile row delta + 1, 28..29 tile column delta + 1
-constexpr D8gEdges d8g_edges() {
-  D8gEdges E{};
-  for (int ph7 = 0; ph7 < 4; ++ph7) {
-    const int py7 = ph7 >> 1, px7 = ph7 & 1;
-    const int rye = py7 ? 0 : 8, rxe = px7 ? 0 : 8;
-    const int dty = py7 ? -1 : 1, dtx = px7 ? -1 : 1;
-    const int ly_e = py7 ? 7 : 0, lx_e = px7 ? 7 : 0;
-    for (int ph8 = 0; ph8 < 4; ++ph8) {
-      const int py8 = ph8 >> 1, px8 = ph8 & 1;
-      for (int iy = 0; iy < 2 + py8; ++iy)
-        for (int ix = 0; ix < 2 + px8; ++ix) {
-          const int t = D8G_TB[ph8] + iy * (2 + px8) + ix;
-          const bool row = iy == (py7 ? 0 : 2), col = ix == (px7 ? 0 : 2);
-          auto add = [&](int ry, int rx, int dy, int dx, int ly, int lx) {
-            E.e[E.n++] = (unsigned)(((ph7 * 25 + t) * 9 + ry) * 9 + rx) | (unsigned)(t * 64 + ly * 8 + lx) << 13 |
-                         (unsigned)ph7 << 24 | (unsigned)(dy + 1) << 26 | (unsigned)(dx + 1) << 28;
-          };
-          if (row)
-            for (int lx = 0; lx < 8; ++lx) add(rye, lx + px7, dty, 0, ly_e, lx);
-          if (col)
-            for (int ly = 0; ly < 8; ++ly) add(ly + py7, rxe, 0, dtx, ly, lx_e);
-          if (row && col) add(rye, rxe, dty, dtx, ly_e, lx_e);
-        }
-    }
-  }
-  return E;
-}
-constexpr D8gEdges kD8gEdges = d8g_edges();
-static_assert(kD8gEdges.n == 489 && kD8gEdges.n <= D8G_EDGE_MAX, "edge list");
-__constant__ unsigned c_d8g_edges[D8G_EDGE_MAX];
-constexpr int D8G_EDGES_PER_THREAD = (kD8gEdges.n + 255) / 256;
-constexpr int D8G_CENTRAL_PER_THREAD = (4 * 25 * 16 + 255) / 256;  // float4 of the 4 phase tiles
-
-constexpr int floordiv2(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
-
-// sums of one plane for a thread at coarse position (2 ay + PY, 2 ax + PX) of the block
-template <int PY, int PX>
-__device__ __forceinline__ void d8g_sum(const float* S, int base, float (&acc)[4]) {
-  static_for<4>([&](auto ph8c) {
-    constexpr int ph8 = decltype(ph8c)::value, py8 = ph8 >> 1, px8 = ph8 & 1;
-    static_for<2 + py8>([&](auto iyc) {
-      constexpr int iy = decltype(iyc)::value;
-      static_for<2 + px8>([&](auto ixc) {
-        constexpr int ix = decltype(ixc)::value;
-        constexpr int t = D8G_TB[ph8] + iy * (2 + px8) + ix;
-        constexpr int py7 = (PY + 1 + iy) & 1, px7 = (PX + 1 + ix) & 1;
-        constexpr int RY = floordiv2(PY - 1 + iy) + py7, RX = floordiv2(PX - 1 + ix) + px7;
-        constexpr int C = ((py7 * 2 + px7) * 25 + t) * 81 + RY * 9 + RX;
-        acc[ph8] = __fadd_rn(acc[ph8], S[base + C]);
-      });
-    });
-  });
-}
-
-__global__ __launch_bounds__(256) void dconv8_gather_lds_kernel(Dconv8Args a) {
-  __shared__ float S[D8G_S];
-  // XCD-contiguous (image, tile) ranges, as dconv8_gather_kernel
-  const int gx = gridDim.x, total = gx * gridDim.y, L = blockIdx.y * gx + blockIdx.x;
-  const int T = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
-  const int n = T / gx, tb = T - n * gx;
-  const int ty = tb / a.tiles_x7, tx = tb - ty * a.tiles_x7;
-  const int h2 = a.H >> 1, w2 = a.W >> 1;  // dconv7's coarse grid (per phase)
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const unsigned plane_floats = 4u * a.tiles_y7 * a.tiles_x7 * (25u * 64u);
-  const unsigned tile_stride = 25u * 64u;
-
-  // this thread's central float4s: q = tid + 256 k -> phase q / 400, tap, row, 4 columns
-  unsigned c_off[D8G_CENTRAL_PER_THREAD];
-  int c_lds[D8G_CENTRAL_PER_THREAD], c_lim[D8G_CENTRAL_PER_THREAD];
-#pragma unroll
-  for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k) {
-    const int q = tid + 256 * k;
-    const int ph7 = q / 400, r = q - ph7 * 400, t = r >> 4, w = r & 15, ly = w >> 1, lx0 = (w & 1) * 4;
-    const bool ok = q < 1600 && 8 * ty + ly < h2;
-    c_off[k] = ok ? ((unsigned)((ph7 * a.tiles_y7 + ty) * a.tiles_x7 + tx) * tile_stride + (unsigned)(t * 64 + ly * 8 + lx0)) * 4u
-                  : kDmaOOR;
-    c_lds[k] = q < 1600 ? ((ph7 * 25 + t) * 9 + ly + (ph7 >> 1)) * 9 + lx0 + (ph7 & 1) : -1;
-    c_lim[k] = w2 - (8 * tx + lx0);  // columns j < c_lim are inside the image
-  }
-  unsigned e_off[D8G_EDGES_PER_THREAD];
-  int e_lds[D8G_EDGES_PER_THREAD];
-#pragma unroll
-  for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k) {
-    const int i = tid + 256 * k;
-    e_lds[k] = -1;
-    e_off[k] = kDmaOOR;
-    if (i < kD8gEdges.n) {
-      const unsigned e = c_d8g_edges[i];
-      const int ph7 = (e >> 24) & 3, ety = ty + (int)((e >> 26) & 3) - 1, etx = tx + (int)((e >> 28) & 3) - 1;
-      const int so = (e >> 13) & 2047, ly = (so >> 3) & 7, lx = so & 7;
-      e_lds[k] = (int)(e & 8191);
-      if ((unsigned)ety < (unsigned)a.tiles_y7 && (unsigned)etx < (unsigned)a.tiles_x7 && 8 * ety + ly < h2 &&
-          8 * etx + lx < w2)
-        e_off[k] = ((unsigned)((ph7 * a.tiles_y7 + ety) * a.tiles_x7 + etx) * tile_stride + (unsigned)so) * 4u;
-    }
-  }
-
-  f32x4 cv[D8G_CENTRAL_PER_THREAD];
-  float ev[D8G_EDGES_PER_THREAD];
-  auto load_plane = [&](int type) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.proj + (size_t)(type * a.nimg + n) * plane_floats), (short)0, (int)(plane_floats * 4u), kBufWord3);
-#pragma unroll
-    for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k)
-      cv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, c_off[k], 0, 0));
-#pragma unroll
-    for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k)
-      ev[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, e_off[k], 0, 0));
-  };
-
-  // this thread's output position: wave = parity class, lane = 8 x 8 at stride 2
-  const int PYw = wave >> 1, PXw = wave & 1, ay = lane >> 3, ax = lane & 7;
-  const int my = 16 * ty + 2 * ay + PYw, mx = 16 * tx + 2 * ax + PXw;
-  const int base = ay * 9 + ax;
-  float outv[3][4];
-  load_plane(0);
-#pragma unroll
-  for (int type = 0; type < 3; ++type) {
-    if (type > 0) __syncthreads();  // the previous plane's sums are done with S
-#pragma unroll
-    for (int k = 0; k < D8G_CENTRAL_PER_THREAD; ++k)
-      if (c_lds[k] >= 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) S[c_lds[k] + j] = j < c_lim[k] ? cv[k][j] : 0.f;
-      }
-#pragma unroll
-    for (int k = 0; k < D8G_EDGES_PER_THREAD; ++k)
-      if (e_lds[k] >= 0) S[e_lds[k]] = ev[k];
-    __syncthreads();
-    if (type < 2) load_plane(type + 1);  // in flight while this plane is summed
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (PYw == 0 && PXw == 0) d8g_sum<0, 0>(S, base, acc);  // wave-uniform branches
-    else if (PYw == 0) d8g_sum<0, 1>(S, base, acc);
-    else if (PXw == 0) d8g_sum<1, 0>(S, base, acc);
-    else d8g_sum<1, 1>(S, base, acc);
-    const float b = a.bias[type > 0 ? 1 : 0];
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) outv[type][ph] = clip01(leaky02(__fadd_rn(acc[ph], b)));
-  }
-  if (my < a.H && mx < a.W) d8_store_rgb(a, n, my, mx, outv);
-}
-
-// ------------------------------------------------------------------------------------
-// dconv8 on the matrix pipe (split-f16, v_mfma_f32_16x16x32_f16), fused with the inverse
-// colour transform and quantiser.  Per 16 coarse positions (one row segment) and plane:
-//   D[phase][px] = sum over 9 halo neighbours d and 2 channel chunks c of A_dc x B_dc,
-//   A_dc[phase][ci] = w[tap(phase, d)][32c + ci] (0 where the phase does not use d; rows
-//   4..15 are zero), B_dc[ci][px] = x[px + d][32c + ci]
-// = 18 x 3 MFMAs.  The A fragments (weights, 36 x 16 B per lane) stay in VGPRs for a
-// whole plane; B fragments are conflict-free ds_read_b128 from 160-B pixel records
-// [hi 32 ch | lo 32 ch | pad] (10 slots: every 16-lane group hits 16 distinct slots).
-// Lanes 0..15 receive D rows 0..3 = the four phases of their pixel.
-// Block = 4 waves = 8 x 32 coarse positions of one image; wave w owns rows 2w, 2w+1.
-// ------------------------------------------------------------------------------------
-constexpr int D8M_PSB = 160;
-constexpr int D8M_HALO = (D8_HH * D8_HW * D8M_PSB + 4095) / 4096 * 4096;  // whole DMA rounds (57,344 B)
-constexpr int D8M_RES = 3 * D8_TH * D8_TW * 4 * 4;  // per-plane phase results, 12,288 B
-
-__global__ __launch_bounds__(256, 2) void dconv8_x3_kernel(Dconv8Args a) {
-  __shared__ __attribute__((aligned(16))) char halo[D8M_HALO + D8M_RES];
-  f32x4* res = (f32x4*)(halo + D8M_HALO);  // [plane][8 rows][32 cols] x 4 phases
-  const int n = blockIdx.y;
-  const int tyi = blockIdx.x / a.tiles_x;
-  const int t0y = tyi * D8_TH, t0x = (blockIdx.x - tyi * a.tiles_x) * D8_TW;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  // tile i of this wave: row 2*wave + (i>>1), columns (i&1)*16 .. +15
-  int boff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    boff[i] = ((2 * wave + (i >> 1)) * D8_HW + (i & 1) * 16 + (lane & 15)) * D8M_PSB + (lane >> 4) * 16;
-
-#pragma unroll 1
-  for (int type = 0; type < 3; ++type) {
-    const int p = type * a.nimg + n;
-    const int model = type > 0 ? 1 : 0;
-    f16x8 A[9][2][2];
-    const f16x8* wa = (const f16x8*)a.wx + (size_t)model * 9 * 2 * 2 * 64 + lane;
-#pragma unroll
-    for (int d = 0; d < 9; ++d)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int hl = 0; hl < 2; ++hl) A[d][c][hl] = wa[((d * 2 + c) * 2 + hl) * 64];
-    f32x4 acc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const char* inb = (const char*)a.in_s + (size_t)p * a.H * a.W * 256;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      __syncthreads();  // previous chunk fully consumed
-      // DMA the 10 x 34 halo of channel chunk c: record slots 0..3 <- hi slots 4c..4c+3,
-      // 4..7 <- lo slots 8+4c.., 8..9 <- zeros; out-of-image pixels <- zeros
-#if !NIC_DMA_STAGE
-      // 8 record slots per pixel (hi 4c..4c+3, lo 8+4c..), batches of clamped 16-B loads
-      constexpr int TOTAL = D8_HH * D8_HW * 8, ITER = (TOTAL + 255) / 256, BATCH = 7;
-#pragma unroll
-      for (int it0 = 0; it0 < ITER; it0 += BATCH) {
-        u32x4 v[BATCH];
-        bool inside[BATCH];
-#pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          if (it0 + b >= ITER) break;
-          const int idx = min((int)threadIdx.x + (it0 + b) * 256, TOTAL - 1);
-          const int pix = idx >> 3, k = idx & 7;
-          const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
-          const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
-          inside[b] = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-          const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-          const int gslot = k < 4 ? 4 * c + k : 8 + 4 * c + (k - 4);
-          v[b] = *(const u32x4*)(inb + ((size_t)cy * a.W + cx) * 256 + gslot * 16);
-        }
-#pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          if (it0 + b >= ITER) break;
-          const int idx = threadIdx.x + (it0 + b) * 256;
-          if (idx < TOTAL)
-            *(u32x4*)(halo + (idx >> 3) * D8M_PSB + (idx & 7) * 16) = inside[b] ? v[b] : (u32x4){0u, 0u, 0u, 0u};
-        }
-      }
-#else
-      constexpr int SLOTS = D8_HH * D8_HW * 10;
-#pragma unroll 2
-      for (int q0 = wave * 64; q0 < SLOTS; q0 += 256) {
-        const int q = q0 + lane;
-        const int pix = q / 10, k = q - pix * 10;
-        const int hy = pix / D8_HW, hx = pix - hy * D8_HW;
-        const int gy = t0y - 1 + hy, gx = t0x - 1 + hx;
-        const bool valid = q < SLOTS && k < 8 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-        const int gslot = k < 4 ? 4 * c + k : 8 + 4 * c + (k - 4);
-        const char* src = valid ? inb + ((size_t)gy * a.W + gx) * 256 + gslot * 16 : a.zero16;
-        dma16(src, halo + q0 * 16);
-      }
-      dma_wait_all();
-#endif
-      __syncthreads();
-#pragma unroll
-      for (int d = 0; d < 9; ++d) {
-        const int doff = ((d / 3) * D8_HW + (d % 3)) * D8M_PSB;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f16x8 bhi = *(const f16x8*)(halo + boff[i] + doff);
-          const f16x8 blo = *(const f16x8*)(halo + boff[i] + doff + 64);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][1], bhi, acc[i], 0, 0, 0);  // w_lo*a_hi
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], blo, acc[i], 0, 0, 0);  // w_hi*a_lo
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], bhi, acc[i], 0, 0, 0);  // w_hi*a_hi
-        }
-      }
-    }
-    const float scale = a.wscale[model], b = a.bias[model];
-    if (lane < 16) {  // D rows 0..3 (the phases) live in lanes 0..15
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f32x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(scale_bias(acc[i][r], scale, b)));
-        res[(type * D8_TH + 2 * wave + (i >> 1)) * D8_TW + (i & 1) * 16 + lane] = v;
-      }
-    }
-  }
-  __syncthreads();
-
-  // epilogue: one thread per coarse position, 4 output pixels x RGB
-  const int ty = threadIdx.x / D8_TW, tx = threadIdx.x % D8_TW;
-  const int my = t0y + ty, mx = t0x + tx;
-  if (my >= a.H || mx >= a.W) return;
-  const f32x4 yv = res[(0 * D8_TH + ty) * D8_TW + tx];
-  const f32x4 cbv = res[(1 * D8_TH + ty) * D8_TW + tx];
-  const f32x4 crv = res[(2 * D8_TH + ty) * D8_TW + tx];
-  const int OW = a.W * 2;
-#pragma unroll
-  for (int py = 0; py < 2; ++py) {
-    uint8_t rgb[6];
-    float rgbf[6];
-#pragma unroll
-    for (int px = 0; px < 2; ++px) {
-      const int ph = py * 2 + px;
-      const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
-      const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
-      const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
-        rgbf[px * 3 + ch] = v;
-        rgb[px * 3 + ch] = quant255(v);
-      }
-    }
-    const size_t o = (((size_t)n * a.H * 2 + 2 * my + py) * OW + 2 * mx) * 3;
-    uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
-    d16[0] = rgb[0] | (rgb[1] << 8);
-    d16[1] = rgb[2] | (rgb[3] << 8);
-    d16[2] = rgb[4] | (rgb[5] << 8);
-    if (a.out_f32) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// dconv8 as a strip walk (split-f16 MFMA, same A fragments and D layout as dconv8_x3).
-// A block owns a 16-wide strip of coarse columns of one image (all three planes) over a
-// segment of rows, and walks it top to bottom: every input row is fetched from HBM once
-// (plus a 2-column halo), into an R-row LDS ring by LDS-DMA (every wave issues a quarter of
-// each row's pieces; R-3 rows in flight), while three MFMA waves -- one per plane, weights
-// resident -- compute output row y from ring rows y-1..y+1.  Their clipped phase values
-// meet in LDS and the fourth wave runs the inverse colour transform + quantiser of row y-1.
-// LDS row slot: [plane][18 px][16 slots of 16 B] = the HBM pixel record [hi 64 | lo 64]
-// with slot s stored at s ^ (2 px & 15): the B-fragment reads (lane (g, l16) = pixel
-// l16 + dx, slot 4c + g [+ 8]) then hit 16 distinct slots per ds_read_b128 group for every
-// neighbour column dx (exhaustive search; s ^ (px & 15) collides for odd dx), no padding.
-// ------------------------------------------------------------------------------------
-#ifndef NIC_D8S_R
-#define NIC_D8S_R 5
-#endif
-constexpr int D8S_W = 16;                                 // coarse columns per strip
-constexpr int D8S_PX = D8S_W + 2;                         // with the halo columns
-constexpr int D8S_ROW = 3 * D8S_PX * 256;                 // 13,824 B of data per ring row
-constexpr int D8S_PIECES = (D8S_ROW + 1023) / 1024;       // 14 DMA wave-instructions per row
-constexpr int D8S_SLOT = D8S_PIECES * 1024;               // ring row stride
-constexpr int D8S_R = NIC_D8S_R;                          // ring rows
-constexpr int D8S_EX = 2 * 3 * D8S_W * 16;                // phase exchange, double-buffered
-constexpr int D8S_VMC = (D8S_R - 4) * D8S_PIECES;         // DMA pieces younger than row y+2
-static_assert(D8S_R >= 5 && D8S_VMC <= 63, "ring depth vs the 6-bit vmcnt");
-
-__global__ __launch_bounds__(256, 2) void dconv8_strip_kernel(Dconv8Args a) {
-  __shared__ __attribute__((aligned(16))) char lds[D8S_R * D8S_SLOT + D8S_EX];
-  f32x4* ex = (f32x4*)(lds + D8S_R * D8S_SLOT);  // [row parity][plane][16 px] x 4 phases
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-  int b = blockIdx.x;
-  const int seg = b % a.nseg;
-  b /= a.nseg;
-  const int strip = b % a.strips, n = b / a.strips;
-  const int x0 = strip * D8S_W;
-  const int r0 = seg * a.seg_rows, r1 = min(a.H, r0 + a.seg_rows);
-  const size_t plane_bytes = (size_t)a.H * a.W * 256;
-
-  // ---- loading, shared by the four waves: wave w DMAs pieces w, w+4, ... of every row ----
-  // piece k: LDS slot q = 64k + lane -> (plane, px, stored slot s'); source = HBM slot
-  // s' ^ (2 px & 15) of pixel (row, x0 - 1 + px) of that plane
-  constexpr int NPW = (D8S_PIECES + 3) / 4;
-  const int npw = (D8S_PIECES - wave + 3) / 4;  // this wave's pieces per row (NPW or NPW-1)
-  long long src[NPW];
-#pragma unroll
-  for (int j = 0; j < NPW; ++j) {
-    const int q = 64 * (wave + 4 * j) + lane;
-    const int pl = q / (D8S_PX * 16), r = q - pl * (D8S_PX * 16);
-    const int px = r >> 4, s = (r & 15) ^ ((2 * px) & 15);
-    const int gx = x0 - 1 + px;
-    src[j] = (q < 3 * D8S_PX * 16 && gx >= 0 && gx < a.W)
-                 ? (long long)(pl * a.nimg + n) * plane_bytes + (long long)gx * 256 + s * 16
-                 : -1;
-  }
-  auto issue_row = [&](int row) {
-    char* dst = lds + ((row + D8S_R) % D8S_R) * D8S_SLOT;
-    const bool rin = row >= 0 && row < a.H;
-    const long long roff = (long long)row * a.W * 256;
-#pragma unroll
-    for (int j = 0; j < NPW; ++j) {
-      if (j == NPW - 1 && npw < NPW) break;  // wave-uniform
-      const char* s = (rin && src[j] >= 0) ? (const char*)a.in_s + roff + src[j] : a.zero16;
-      dma16(s, dst + (wave + 4 * j) * 1024);
-    }
-  };
-  // row y+2 landed: all but this wave's pieces of rows y+3 .. y+R-2 are done
-  auto wait_row = [&]() {
-    if (npw == NPW)
-      __builtin_amdgcn_s_waitcnt(0x0F70 | ((NPW * (D8S_R - 4)) & 15) | (((NPW * (D8S_R - 4)) >> 4) << 14));
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70 | (((NPW - 1) * (D8S_R - 4)) & 15) | ((((NPW - 1) * (D8S_R - 4)) >> 4) << 14));
-  };
-  // prologue: rows r0-1 .. r0+1 landed, r0+2 .. r0+R-3 in flight
-  issue_row(r0 - 1);
-  issue_row(r0);
-  issue_row(r0 + 1);
-  dma_wait_all();
-#pragma unroll
-  for (int k = 2; k <= D8S_R - 3; ++k) issue_row(r0 + k);
-
-  if (wave == 3) {
-    // ---- colour epilogue wave: row y-1 from the phase exchange, stores after its vmcnt
-    // wait so that they are older than the next rows' pieces ----
-    for (int y = r0; y <= r1; ++y) {
-      stage_barrier();  // B_y: rows y-1..y+1 complete; ex[(y-1)&1] holds row y-1
-      if (y < r1) issue_row(y + D8S_R - 2);
-      const int ry = y - 1, px = l16, py = g, mx = x0 + px;
-      const bool act = y > r0 && lane < 32 && mx < a.W;
-      uint8_t rgb[6];
-      float rgbf[6];
-      if (act) {
-        const f32x4* e = ex + ((ry & 1) * 3) * D8S_W;
-        const f32x4 yv = e[px], cbv = e[D8S_W + px], crv = e[2 * D8S_W + px];
-#pragma unroll
-        for (int phx = 0; phx < 2; ++phx) {
-          const int ph = py * 2 + phx;
-          const float t0 = __fsub_rn(yv[ph], c_ycbcr_off[0]);
-          const float t1 = __fsub_rn(cbv[ph], c_ycbcr_off[1]);
-          const float t2 = __fsub_rn(crv[ph], c_ycbcr_off[2]);
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {
-            const float v = clip01(project(c_ycbcr_inv + 3 * ch, t0, t1, t2));
-            rgbf[phx * 3 + ch] = v;
-            rgb[phx * 3 + ch] = quant255(v);
-          }
-        }
-      }
-      lds_reads_done();
-      if (y < r1) wait_row();
-      if (act) {
-        const size_t o = (((size_t)n * a.H * 2 + 2 * ry + py) * (a.W * 2) + 2 * mx) * 3;
-        uint16_t* d16 = (uint16_t*)(a.out_u8 + o);
-        d16[0] = rgb[0] | (rgb[1] << 8);
-        d16[1] = rgb[2] | (rgb[3] << 8);
-        d16[2] = rgb[4] | (rgb[5] << 8);
-        if (a.out_f32) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) a.out_f32[o + k] = rgbf[k];
-        }
-      }
-    }
-    dma_wait_all();  // no LDS-DMA outlives the wave
-    return;
-  }
-
-  // ---- MFMA wave: plane `wave` (0 Y, 1 Cb, 2 Cr) ----
-  const int model = wave > 0 ? 1 : 0;
-  f16x8 A[9][2][2];
-  {
-    const f16x8* wa = (const f16x8*)a.wx + (size_t)model * 9 * 2 * 2 * 64 + lane;
-#pragma unroll
-    for (int d = 0; d < 9; ++d)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int hl = 0; hl < 2; ++hl) A[d][c][hl] = wa[((d * 2 + c) * 2 + hl) * 64];
-  }
-  const float scale = a.wscale[model], bias = a.bias[model];
-  // B-fragment offsets inside a ring row: plane `wave`, pixel l16 + dx, slot (8hl + 4c + g)
-  int boff[3][2][2];
-#pragma unroll
-  for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
-        const int px = l16 + dx;
-        boff[dx][c][hl] = (wave * D8S_PX + px) * 256 + (((8 * hl + 4 * c + g) ^ ((2 * px) & 15)) * 16);
-      }
-#ifdef NIC_STAMPS
-  unsigned long long sb = 0, si = 0, sm = 0, sw = 0, t0, t1, t2, t3, t4;
-  NIC_PNOW(t4);
-#endif
-  for (int y = r0; y <= r1; ++y) {
-#ifdef NIC_STAMPS
-    NIC_PNOW(t0);
-#endif
-    stage_barrier();  // B_y
-#ifdef NIC_STAMPS
-    NIC_PNOW(t1);
-    sb += t1 - t0;
-#endif
-    if (y == r1) break;
-    issue_row(y + D8S_R - 2);
-#ifdef NIC_STAMPS
-    NIC_PNOW(t2);
-    si += t2 - t1;
-#endif
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    // 18 groups (dy, c, dx), B fragments read three groups ahead of their MFMAs
-    const char* rows[3];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) rows[dy] = lds + ((y - 1 + dy + D8S_R) % D8S_R) * D8S_SLOT;
-    constexpr int NG = 18, DEPTH = 3;
-    f16x8 fb[DEPTH][2];
-    auto rd = [&](int gi, f16x8(&f)[2]) {
-      const int dy = gi / 6, c = (gi / 3) & 1, dx = gi % 3;
-      f[0] = *(const f16x8*)(rows[dy] + boff[dx][c][0]);
-      f[1] = *(const f16x8*)(rows[dy] + boff[dx][c][1]);
-    };
-#pragma unroll
-    for (int gi = 0; gi < DEPTH; ++gi) rd(gi, fb[gi]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int gi = 0; gi < NG; ++gi) {
-      const int dy = gi / 6, c = (gi / 3) & 1, dx = gi % 3, d = dy * 3 + dx;
-      f16x8(&cur)[2] = fb[gi % DEPTH];
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][1], cur[0], acc, 0, 0, 0);  // w_lo*a_hi
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], cur[1], acc, 0, 0, 0);  // w_hi*a_lo
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[d][c][0], cur[0], acc, 0, 0, 0);  // w_hi*a_hi
-      if (gi + DEPTH < NG) rd(gi + DEPTH, cur);
-      __builtin_amdgcn_sched_barrier(0);  // keep the reads DEPTH groups ahead
-    }
-    if (lane < 16) {  // D rows 0..3 (the phases) of pixel l16
-      f32x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = clip01(leaky02(scale_bias(acc[r], scale, bias)));
-      ex[((y & 1) * 3 + wave) * D8S_W + l16] = v;
-    }
-    lds_reads_done();
-#ifdef NIC_STAMPS
-    NIC_PNOW(t3);
-    sm += t3 - t2;
-#endif
-    wait_row();
-#ifdef NIC_STAMPS
-    NIC_PNOW(t4);
-    sw += t4 - t3;
-#endif
-  }
-  dma_wait_all();
-#ifdef NIC_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = g_stamps + (blockIdx.x * 4 + wave) * 4;
-    o[0] = sb;
-    o[1] = si;
-    o[2] = sm;
-    o[3] = sw;
-  }
-#endif
-}
 
 // ------------------------------------------------------------------------------------
 // Histogram entropy (tf1_13/src/training.py:66-71) and bitstream pack/unpack
@@ -4724,17 +3306,10 @@ hipError_t launch_fp32_chain(const Fp32Chain& chain, hipStream_t st) {
   return hipGetLastError();
 }
 
+// grid of the fp32 one-tile-per-block launches: 8 blocks per CU, 1 for a gated re-run (NIC_CHAIN=0),
+// which exits at its gate unless the split pass tripped (a smaller grid drains faster)
 static int fp32_grid(const RangeGuard& rg, long long jobs) {
-  static const int gated_per_cu = [] {
-    const char* e = std::getenv("NIC_GATE_GRID");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  static const int gated_blocks = [] {  // A/B: absolute block count of the gated grids
-    const char* e = std::getenv("NIC_GATE_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 0;
-  }();
-  if (rg.gate && gated_blocks) return (int)std::min<long long>(jobs, gated_blocks);
-  return (int)std::min<long long>(jobs, (long long)(rg.gate ? gated_per_cu : 8) * device_cus());
+  return (int)std::min<long long>(jobs, (long long)(rg.gate ? 1 : 8) * device_cus());
 }
 
 template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int IN_MODE,
@@ -4786,29 +3361,6 @@ hipError_t launch_layer(LayerId id, const ConvArgs& a, hipStream_t st) {
 }
 
 
-template <int CIN, int COUT, int KS, int S, bool TR, int TH, int TW, int WM, int WN, int WK, int MTW, int IN_MODE,
-          int OUT_MODE, bool RESID>
-static hipError_t launch_x3(ConvArgs a, hipStream_t st) {
-  const int gy = TR ? a.H : a.OH, gx = TR ? a.W : a.OW;
-  const int tiles_y = (gy + TH - 1) / TH;
-  a.tiles_x = (gx + TW - 1) / TW;
-  dim3 grid(tiles_y * a.tiles_x, a.P);
-  hipLaunchKernelGGL(
-      (conv_x3_kernel<CIN, COUT, KS, S, TR, TH, TW, WM, WN, WK, MTW, IN_MODE, OUT_MODE, RESID>), grid,
-      dim3(64 * WM * WN * WK), 0, st, a);
-  return hipGetLastError();
-}
-
-// NIC_WS=0 selects the one-tile-per-block kernels for the 3x3 layers instead of the
-// weight-stationary ones (A/B)
-static bool use_ws() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_WS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static int device_cus() {
   static int cache[64] = {};
   int d = 0;
@@ -4819,46 +3371,6 @@ static int device_cus() {
     cache[d] = n;
   }
   return cache[d];
-}
-
-// Resident blocks per CU of the stride-1 weight-stationary launches (51 KB LDS, <= 128
-// VGPRs: up to 3 fit); NIC_WS_BPC overrides for A/B runs.
-static int ws_k3_blocks_per_cu() {
-  static const int v = [] {
-    const char* e = getenv("NIC_WS_BPC");
-    const int n = e ? atoi(e) : 2;
-    return n >= 1 && n <= 3 ? n : 2;
-  }();
-  return v;
-}
-
-// Per-tile cost of the dconv7 phase groups beyond their MFMA work, in units of half a tap
-// (the projection's 12 MFMAs are one unit; the epilogue, halo issue and barriers add the
-// rest); NIC_D7_C overrides for A/B runs.
-static int ws_proj_cost() {
-  static const int v = [] {
-    const char* e = getenv("NIC_D7_C");
-    const int n = e ? atoi(e) : 1;
-    return n >= 0 && n <= 64 ? n : 1;
-  }();
-  return v;
-}
-
-static bool d7_grouped() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_D7");
-    return e && e[0] == 'g';
-  }();
-  return on;
-}
-
-// NIC_WSX=0: weight-stationary blocks take their groups in blockIdx order (A/B of the XCD remap)
-static bool ws_xcd_remap() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_WSX");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 // Weight-stationary launch: 2 resident blocks per CU, split into groups (tap set, model)
@@ -4874,19 +3386,16 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
   // HaloDma: 32-bit plane offsets, out-of-range slots past the plane (kDmaOOR)
   if ((long long)a.H * a.W * CIN * 4 >= (1LL << 30)) return hipErrorInvalidValue;
   a.ntiles = (int)nt;
-  // transposed layers: one block group per model, every block runs the four phases
-  // (default), or per-phase groups (NIC_D7=g, A/B)
-  const int nset = TRP && d7_grouped() ? 4 : 1;
-  const int taps[4] = {TRP ? (nset == 4 ? 4 : 25) : 9, 6, 6, 9};
+  // one block group per model (transposed layers: every block runs the four phases over its
+  // tiles; per-phase groups measured 6 % slower)
   a.ws_taps = TRP ? 25 : 9;
-  a.ws_ngrp = 2 * nset;
-  long long work[8], total = 0;
-  for (int gi = 0; gi < a.ws_ngrp; ++gi) {
-    const long long planes = (gi & 1) ? a.P - a.nimg : a.nimg;
-    work[gi] = planes * per_plane * (2 * taps[gi >> 1] + (PROJ ? ws_proj_cost() : 0));
+  a.ws_ngrp = 2;
+  long long work[2], total = 0;
+  for (int gi = 0; gi < 2; ++gi) {
+    work[gi] = ((gi & 1) ? a.P - a.nimg : a.nimg) * per_plane;
     total += work[gi];
   }
-  const int target = (TRP ? 2 : ws_k3_blocks_per_cu()) * device_cus();
+  const int target = 2 * device_cus();  // 2 resident blocks per CU
   a.ws_blk[0] = 0;
   for (int gi = 0; gi < a.ws_ngrp; ++gi) {
     const long long tiles = ((gi & 1) ? a.P - a.nimg : a.nimg) * per_plane;
@@ -4894,7 +3403,7 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
     b = b < 1 ? 1 : b > tiles ? tiles : b;
     a.ws_blk[gi + 1] = a.ws_blk[gi] + (int)b;
   }
-  a.ws_xcd = ws_xcd_remap();
+  a.ws_xcd = 1;
   hipLaunchKernelGGL((conv_ws_kernel<CIN, COUT, TH, TW, RESID, TRP, PROJ>), dim3(a.ws_blk[a.ws_ngrp]),
                      dim3(64 * (COUT / 16)), 0, st, a);
   return hipGetLastError();
@@ -4904,16 +3413,12 @@ static hipError_t launch_ws(ConvArgs a, hipStream_t st) {
 // (the part of its range inside one (plane, strip) column of H rows) on top of one step per row:
 // equal-row ranges give the blocks that straddle a plane boundary 2 segments (config 2: 48 rows
 // = 54 steps against 51 for a one-segment block).  Greedy ranges under a step budget T, the
-// smallest T that fits the grid (binary search), even that out.  NIC_K3P_BAL = the per-segment
-// cost the budget charges, in steps (default 2: pair 0.2379-0.2385 ms vs 0.2388-0.2402 at 3,
-// 0.2392-0.2404 at 4 and 0.2415-0.2423 for the equal-rows split, NIC_K3P_BAL=0; same box).
+// smallest T that fits the grid (binary search), even that out.  F = the per-segment cost the
+// budget charges, in steps (2: pair 0.2379-0.2385 ms vs 0.2388-0.2402 at 3, 0.2392-0.2404 at 4
+// and 0.2415-0.2423 for the equal-rows split; same box, profiles/r4_ab_logs.txt).
 static void k3pair_balance(long long total, int H, int G, K3Ranges& r) {
-  static const int F = [] {
-    const char* e = getenv("NIC_K3P_BAL");
-    const int v = e ? atoi(e) : 2;
-    return v >= 0 && v <= 64 ? v : 2;
-  }();
-  if (F == 0 || G <= 0 || G > K3P_MAX_GRID || total >= (1LL << 31) || H <= 0) return;
+  constexpr int F = 2;
+  if (G <= 0 || G > K3P_MAX_GRID || total >= (1LL << 31) || H <= 0) return;
   // blocks the greedy needs under budget T (stops counting past G); fills r when `write`
   auto fill = [&](long long T, bool write) {
     long long s = 0;
@@ -4954,23 +3459,15 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
   a.tiles_x = k3pair_strips(a.W);
   const long long rows = (long long)a.P * a.tiles_x * a.H;
   if (rows == 0) return hipSuccess;
-  // at most one block per CU, at least `sr` rows per block (NIC_K3P_SR, default 4): a block's
-  // fixed cost is 3 pipeline fill steps and 2 recomputed conv_a rows, so small batches (the
-  // host surface's chunks: 11-21 images) are faster spread over every CU with few rows each
-  // than on fewer CUs with more (16 rows per block left 124 of 256 CUs idle at 11 images)
-  static const int sr = [] {
-    const char* e = getenv("NIC_K3P_SR");
-    const int v = e ? atoi(e) : 4;
-    return v >= 1 && v <= 64 ? v : 4;
-  }();
+  // at most one block per CU, at least 4 rows per block: a block's fixed cost is 3 pipeline fill
+  // steps and 2 recomputed conv_a rows, so small batches (the host surface's chunks: 11-21
+  // images) are faster spread over every CU with few rows each than on fewer CUs with more (16
+  // rows per block left 124 of 256 CUs idle at 11 images)
+  constexpr int sr = 4;
   const int grid = (int)std::max(1LL, std::min<long long>((rows + sr - 1) / sr, device_cus()));
   const int mt = (a.W + 15) / 16;
-  // SKEW (default; NIC_K3P_SK=0 for the lockstep order): conv_b runs each row's epilogue at the
-  // start of the next step, beside conv_a's MFMA stream, instead of after its own stream
-  static const bool sk = [] {
-    const char* e = getenv("NIC_K3P_SK");
-    return !(e && e[0] == '0');
-  }();
+  // SKEW: conv_b runs each row's epilogue at the start of the next step, beside conv_a's MFMA
+  // stream, instead of after its own stream (the lockstep order measured 1.3 % slower)
   K3Ranges rng;
   rng.start[0] = -1;
   k3pair_balance(rows, a.H, grid, rng);
@@ -4988,18 +3485,8 @@ hipError_t launch_k3pair_x3(const ConvArgs& a0, hipStream_t st) {
       }
     }
   };
-  sk ? pick(std::true_type{}) : pick(std::false_type{});
+  pick(std::true_type{});
   return hipGetLastError();
-}
-
-// XCD-contiguous tile positions in the k5 s2 forward convs (default; NIC_XCD2=0 for the
-// plain block-strided order): conv12 0.2594 -> 0.2572 ms, conv8 0.0767 -> 0.0758 ms same-box
-static bool ws2_tile_xcd() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_XCD2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 // k5 s2 forward convs: one 8-wave block per CU, split into a Y and a CbCr group in
@@ -5029,7 +3516,9 @@ size_t hist_fold_scratch_bytes(int nimg, int h8, int w8) {  // the counts [3 nim
   return (size_t)3 * nimg * 256 * sizeof(uint32_t);
 }
 
-template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool FUSE1 = false, bool PIPE12 = false>
+// k5 s2 forward convs on the tap-split weight-stationary kernel (conv2 of conv12 with PIPE12,
+// conv8 with the latent histogram fold when a.hist_part is set)
+template <int CIN, int COUT, int NTS, int TH, int OUT_MODE, bool PIPE12 = false>
 static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.tiles_y = (a.OH + TH - 1) / TH;
   a.tiles_x = (a.OW + 7) / 8;
@@ -5045,44 +3534,24 @@ static hipError_t launch_ws2(ConvArgs a, hipStream_t st) {
   a.ws_blk[0] = 0;
   a.ws_blk[1] = by;
   a.ws_blk[2] = by + bc;
-  a.tile_xcd = ws2_tile_xcd() ? 1 : 0;
   if constexpr (PIPE12) {
     hipLaunchKernelGGL(conv12_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
-  } else if constexpr (OUT_MODE == OUT_U8_LATENT && !FUSE1) {
-    static const bool xr = [] {
-      const char* e = getenv("NIC_C8W");
-      return e && e[0] == 'x';
-    }();
-    a.ws2_xrange = xr && !a.hist_part ? 1 : 0;
+  } else if constexpr (OUT_MODE == OUT_U8_LATENT) {
     if (a.hist_part) {
       if (!hist_fold_supported(a.nimg, a.OH, a.OW)) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1, true>), dim3(a.ws_blk[2]), dim3(512), 0,
-                         st, a);
+      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, true>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
     } else {
-      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+      hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
     }
   } else {
-    hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE, FUSE1>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((conv_ws2_kernel<CIN, COUT, NTS, TH, OUT_MODE>), dim3(a.ws_blk[2]), dim3(512), 0, st, a);
   }
   return hipGetLastError();
-}
-
-bool conv12_fused() { return use_ws(); }
-
-// NIC_C12=serial selects the unpipelined fused kernel (conv_ws2_kernel FUSE1: one halo
-// buffer, conv1 between two barriers) for A/B runs
-static bool c12_serial() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_C12");
-    return e && e[0] == 's';
-  }();
-  return on;
 }
 
 hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (!a.rgb || !a.wx1 || !a.bias1 || a.H0 <= 0 || a.W0 <= 0) return hipErrorInvalidValue;
-  if (c12_serial()) return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
   if (!a.cplane || a.OH <= 0 || a.OW <= 0) return hipErrorInvalidValue;
   int oy, ox;
   c12_plane_geom(a.OH, a.OW, a.pad_y, a.pad_x, a.p1y, a.p1x, &oy, &ox, &a.cp_h, &a.cp_w);
@@ -5095,69 +3564,52 @@ hipError_t launch_conv12_x3(const ConvArgs& a0, hipStream_t st) {
                      dim3(256), 0, st, a.rgb, a.cplane, a.nimg, a.H0, a.W0, oy, ox, a.cp_h, a.cp_w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true, true>(a, st);
+  return launch_ws2<32, 64, 2, 8, OUT_SPLIT, true>(a, st);
 }
 
-static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st);
-static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st);
-static int dconv1_variant() {
-  static const int v = [] {
-    const char* e = getenv("NIC_D1");
-    // default: all phases per staged tile (dconv1_all_kernel, 0.056-0.057 vs 0.064-0.065 ms for
-    // the per-phase weight-stationary walk, NIC_D1=p, same box: profiles/r4c_*)
-    return !e ? 8 : e[0] == '1' ? 1 : e[0] == 'w' ? (e[1] == '8' ? 3 : 2) : e[0] == 'q' ? 4 : e[0] == 's' ? 5
-                  : e[0] == '8' ? 6 : e[0] == 'x' ? 7 : e[0] == 'a' ? 8 : 0;
-  }();
-  return v;
+// all phases per staged tile: one 8-wave block per CU, blocks split between the models in
+// proportion to their tiles (Y : CbCr = 1 : 2)
+static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
+  a.tiles_y = (a.H + 7) / 8;
+  a.tiles_x = (a.W + 7) / 8;
+  const long long per_plane = (long long)a.tiles_y * a.tiles_x, nt = per_plane * a.P;
+  if (nt == 0) return hipSuccess;
+  if (nt > INT32_MAX || a.P != 3 * a.nimg || a.OH != 2 * a.H || a.OW != 2 * a.W || !a.in_u8) return hipErrorInvalidValue;
+  if ((long long)a.OH * a.OW * 256 >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit granule offsets
+  const long long target = device_cus();
+  const long long ty = (long long)a.nimg * per_plane, tc = 2LL * a.nimg * per_plane;
+  const int by = (int)std::max(1LL, std::min(ty, (target + 1) / 3)), bc = (int)std::max(1LL, std::min(tc, target - by));
+  a.ws_ngrp = 2;
+  a.ws_blk[0] = 0;
+  a.ws_blk[1] = by;
+  a.ws_blk[2] = by + bc;
+  hipLaunchKernelGGL(dconv1_all_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_layer_x3(LayerId id, const ConvArgs& a, hipStream_t st) {
   switch (id) {
-    case L_CONV2:  // 32->64 k5 s2: tap-split weight-stationary, or 8x8 tile, 2 waves split N
-      if (use_ws()) return launch_ws2<32, 64, 2, 8, OUT_SPLIT>(a, st);
-      return launch_x3<32, 64, 5, 2, false, 8, 8, 1, 2, 1, 2, IN_SPLIT, OUT_SPLIT, false>(a, st);
-    case L_CONV3:  // 64->64 k3 s1: 16x16 tiles, 4 stages of 16 channels (+ their weights) by LDS-DMA,
-                   // 8 consumers (2 per SIMD) x 32 px x 64 co, 4 loader waves
-      if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
-    case L_CONV4:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
-    case L_CONV8:  // 64->32 k5 s2 -> latent: tap-split weight-stationary (2 channel groups x 4 tap
-                   // quarters, 4x8 tiles), or 4x8 tile with taps split over 4 waves
-      if (use_ws()) return launch_ws2<64, 32, 4, 4, OUT_U8_LATENT>(a, st);
-      return launch_x3<64, 32, 5, 2, false, 4, 8, 1, 1, 4, 1, IN_SPLIT, OUT_U8_LATENT, false>(a, st);
-    case L_DCONV1:  // latent -> 64, transposed k5 s2: all four phases per staged 8x16 code tile
-                    // (dconv1_all_kernel); NIC_D1=p the per-phase weight-stationary walk, and the
-                    // older one-tile-per-block forms below (A/B)
-      switch (dconv1_variant()) {
-        case 1: return launch_x3<32, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        case 2: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        case 3: return launch_x3<32, 64, 5, 2, true, 16, 16, 4, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        case 4: return launch_x3<32, 64, 5, 2, true, 8, 8, 2, 2, 1, 1, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        case 5: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_LATENT, OUT_SPLIT, false>(a, st);
-        // NIC_D1=8: the 8x8-tile form on codes (0.0785-0.0789 vs 0.0763-0.0765 ms for the
-        // default, same box)
-        case 6: return launch_x3<32, 64, 5, 2, true, 8, 8, 1, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        // NIC_D1=x: the u8 codes as exact f16 activations (2 MFMAs per MAC, 1/255 in the
-        // epilogue; NIC_D1=s the split dequantised activations, 3 MFMAs, round 2) on 8x16
-        // coarse tiles, 4 waves, one tile per block (round-3 default before dconv1_ws_kernel)
-        case 7: return launch_x3<32, 64, 5, 2, true, 8, 16, 2, 2, 1, 2, IN_U8_CODES, OUT_SPLIT, false>(a, st);
-        case 8: return launch_dconv1_all(a, st);
-        default: return launch_dconv1_ws(a, st);
-      }
+    case L_CONV2:  // 32->64 k5 s2 (conv12_kernel runs it fused with conv1; this form is unused there)
+      return launch_ws2<32, 64, 2, 8, OUT_SPLIT>(a, st);
+    case L_CONV3:  // 64->64 k3 s1 weight-stationary (the fused pair takes planes it supports)
     case L_DCONV5:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, false, false>(a, st);
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
+      return launch_ws<64, 64, 8, 8, false, false>(a, st);
+    case L_CONV4:
     case L_DCONV6:
-      if (use_ws()) return launch_ws<64, 64, 8, 8, true, false>(a, st);
-      return launch_x3<64, 64, 3, 1, false, 8, 16, 1, 2, 1, 4, IN_SPLIT_DMA, OUT_SPLIT, true>(a, st);
-    case L_DCONV7:  // 64->64 transposed k5 s2: per-phase weight-stationary groups, or 8x16 coarse tiles
-      if (use_ws()) return launch_ws<64, 64, 8, 8, false, true>(a, st);
-      return launch_x3<64, 64, 5, 2, true, 8, 16, 1, 2, 1, 4, IN_SPLIT, OUT_SPLIT, false>(a, st);
-    default:
+      return launch_ws<64, 64, 8, 8, true, false>(a, st);
+    case L_CONV8:  // 64->32 k5 s2 -> latent: tap-split weight-stationary (2 channel groups x 4 tap
+                   // quarters, 4x8 tiles)
+      return launch_ws2<64, 32, 4, 4, OUT_U8_LATENT>(a, st);
+    case L_DCONV1:  // latent -> 64, transposed k5 s2: all four phases per staged 8x8 code tile
+      return launch_dconv1_all(a, st);
+    default:  // dconv7 runs with dconv8's projections (launch_dconv7_proj_x3)
       return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
+  if (!a.proj || !a.proj_w || a.OH != 2 * a.H || a.OW != 2 * a.W) return hipErrorInvalidValue;
+  return launch_ws<64, 64, 8, 8, false, true, true>(a, st);
 }
 
 hipError_t launch_conv1(Conv1Args a, hipStream_t st) {
@@ -5182,118 +3634,12 @@ hipError_t launch_dconv8(Dconv8Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// dconv8 in f16x3 mode: 'p' (default) projections fused into dconv7 + gather,
-// NIC_D8=strip the strip-walk MFMA kernel, NIC_D8=tile the one-tile-per-block one (A/B)
-static char d8_mode() {
-  static const char m = [] {
-    const char* e = getenv("NIC_D8");
-    return e && (e[0] == 't' || e[0] == 's') ? e[0] : 'p';
-  }();
-  return m;
-}
-static bool use_d8_strip() { return d8_mode() != 't'; }
-
-bool dconv78_fused() { return use_ws() && d8_mode() == 'p'; }
-
-// dconv1 on the u8 codes, persistent weight-stationary (dconv1_ws_kernel): two block groups
-// (Y, CbCr) in proportion to their planes, two blocks per CU
-static hipError_t launch_dconv1_ws(ConvArgs a, hipStream_t st) {
-  a.tiles_y = (a.H + 7) / 8;
-  a.tiles_x = (a.W + 7) / 8;
-  const long long per_plane = (long long)a.tiles_y * a.tiles_x, nt = per_plane * a.P;
-  if (nt == 0) return hipSuccess;
-  if (nt > INT32_MAX || a.P != 3 * a.nimg || a.OH != 2 * a.H || a.OW != 2 * a.W || !a.in_u8) return hipErrorInvalidValue;
-  if ((long long)a.OH * a.OW * 256 >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit granule offsets
-  static const int bpc = [] {  // resident blocks per CU (NIC_D1_BPC; 156 VGPRs allow 3)
-    const char* e = getenv("NIC_D1_BPC");
-    const int v = e ? atoi(e) : 2;
-    return v >= 1 && v <= 3 ? v : 2;
-  }();
-  const long long target = (long long)bpc * device_cus();
-  const long long ty = (long long)a.nimg * per_plane, tc = 2LL * a.nimg * per_plane;
-  const int by = (int)std::max(1LL, std::min(ty, (target + 1) / 3)), bc = (int)std::max(1LL, std::min(tc, target - by));
-  a.ws_ngrp = 2;
-  a.ws_blk[0] = 0;
-  a.ws_blk[1] = by;
-  a.ws_blk[2] = by + bc;
-  hipLaunchKernelGGL(dconv1_ws_kernel, dim3(by + bc), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-// all phases per staged tile: one 8-wave block per CU, blocks split between the models in
-// proportion to their tiles (Y : CbCr = 1 : 2)
-static hipError_t launch_dconv1_all(ConvArgs a, hipStream_t st) {
-  a.tiles_y = (a.H + 7) / 8;
-  a.tiles_x = (a.W + 7) / 8;
-  const long long per_plane = (long long)a.tiles_y * a.tiles_x, nt = per_plane * a.P;
-  if (nt == 0) return hipSuccess;
-  if (nt > INT32_MAX || a.P != 3 * a.nimg || a.OH != 2 * a.H || a.OW != 2 * a.W || !a.in_u8) return hipErrorInvalidValue;
-  if ((long long)a.OH * a.OW * 256 >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit granule offsets
-  const long long target = device_cus();
-  const long long ty = (long long)a.nimg * per_plane, tc = 2LL * a.nimg * per_plane;
-  const int by = (int)std::max(1LL, std::min(ty, (target + 1) / 3)), bc = (int)std::max(1LL, std::min(tc, target - by));
-  a.ws_ngrp = 2;
-  a.ws_blk[0] = 0;
-  a.ws_blk[1] = by;
-  a.ws_blk[2] = by + bc;
-  hipLaunchKernelGGL(dconv1_all_kernel, dim3(a.ws_blk[2]), dim3(512), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_dconv7_proj_x3(const ConvArgs& a, hipStream_t st) {
-  if (!a.proj || !a.proj_w || a.OH != 2 * a.H || a.OW != 2 * a.W) return hipErrorInvalidValue;
-  return launch_ws<64, 64, 8, 8, false, true, true>(a, st);
-}
-
-// NIC_D8G=l: the LDS-staged gather instead of the direct one (A/B: 0.074-0.076 vs
-// 0.072-0.075 ms same-box over 3 rounds, bit-identical results -- not the default)
-static bool d8g_direct() {
-  static const bool on = [] {
-    const char* e = getenv("NIC_D8G");
-    return !(e && e[0] == 'l');
-  }();
-  return on;
-}
-
 hipError_t launch_dconv8_gather(Dconv8Args a, hipStream_t st) {
   if (!a.proj || (a.H & 1) || (a.W & 1)) return hipErrorInvalidValue;
   if (a.tiles_y7 != (a.H / 2 + 7) / 8 || a.tiles_x7 != (a.W / 2 + 7) / 8) return hipErrorInvalidValue;
   const int tiles_y = (a.H + 15) / 16;
   a.tiles_x = (a.W + 15) / 16;
-  if (d8g_direct()) {
-    hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  // one block per dconv7 8x8 tile and image (= 16 x 16 coarse positions of dconv8)
-  static bool uploaded[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  if (!uploaded[dev]) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_d8g_edges), kD8gEdges.e, sizeof(kD8gEdges.e));
-    if (e != hipSuccess) return e;
-    uploaded[dev] = true;
-  }
-  hipLaunchKernelGGL(dconv8_gather_lds_kernel, dim3(a.tiles_y7 * a.tiles_x7, a.nimg), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_dconv8_x3(Dconv8Args a, hipStream_t st) {
-  if (use_d8_strip()) {
-    a.strips = (a.W + D8S_W - 1) / D8S_W;
-    const long long units = (long long)a.nimg * a.strips;
-    // enough row segments for ~2 blocks per CU, each at least 16 rows long
-    int nseg = (int)((2LL * device_cus() + units - 1) / units);
-    nseg = std::max(1, std::min(nseg, a.H / 16));
-    a.seg_rows = (a.H + nseg - 1) / nseg;
-    a.nseg = (a.H + a.seg_rows - 1) / a.seg_rows;
-    const long long grid = units * a.nseg;
-    if (grid > INT32_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(dconv8_strip_kernel, dim3((unsigned)grid), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  const int tiles_y = (a.H + D8_TH - 1) / D8_TH;
-  a.tiles_x = (a.W + D8_TW - 1) / D8_TW;
-  hipLaunchKernelGGL(dconv8_x3_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dconv8_gather_kernel, dim3(tiles_y * a.tiles_x, a.nimg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -5314,32 +3660,24 @@ size_t hist_scratch_bytes(int nimg, int plane_px) {
 
 hipError_t launch_hist(const uint8_t* z, int nimg, int plane_px, uint32_t* part, uint32_t* counts, float* bits,
                        hipStream_t st) {
+  // 1024-thread blocks, 512 of them (2 per CU) with 16 LDS replicas per bin from 24 MB of latent
+  // up, else 256-thread blocks with 8 (>= 48 KB per block: the per-block LDS clear and 768
+  // partial stores amortised).  Measured on 4K x 8 latents (tools/hist_ab.py, round 2):
+  // 16 replicas 21.6 us, 8 25.4, 32 (98 KB, one block per CU) 27.2; a packed-u16 32-replica
+  // layout 15 % slower.  NIC_HIST=big / small forces either form (read per call: the GPU test
+  // runs both on one latent).
   const char* hv = getenv("NIC_HIST");
-  // Default: 1024-thread blocks, 512 of them (2 per CU) with 16 LDS replicas per bin from
-  // 24 MB of latent up, else 256 with 8 (>= 48 KB per block: the per-block LDS clear and 768
-  // partial stores amortised).
-  // A/B switch (tools/hist_ab.py): NIC_HIST=<R>[z] = 256-thread blocks with R replicas
-  // (1536 blocks; 8 replicas measured best, a packed-u16 32-replica layout was 15 % slower),
-  // <R>b<N>[u] = 1024-thread blocks, N x 256 of them (R: 4, 8, g = 16, h = 32; u = 8 loads in
-  // flight).  4K x 8 latents: 16 replicas 21.6 us, 8: 25.4, 32 (98 KB, 1 block per CU): 27.2.
-  const bool big = !hv || hv[1] == 'b';
+  const int force = !hv ? 0 : hv[0] == 'b' ? 1 : hv[0] == 's' ? 2 : 0;
   const long long total = (long long)plane_px * 96 * nimg;
-  const char m = hv ? hv[0] : (total >= (24ll << 20) ? 'g' : '8');
-  const bool zb = hv && hv[1] == 'z';
-  const int bmul = hv && big && hv[2] >= '1' && hv[2] <= '6' ? hv[2] - '0' : (total >= (24ll << 20) ? 2 : 1);
+  const bool big = force ? force == 1 : total >= (24ll << 20);
   int chunk_vec;
-  const int chunks = hist_chunks(nimg, plane_px, &chunk_vec, big ? 256 * bmul : 1536);
-  auto go = [&](auto kern, int nt) {
-    hipLaunchKernelGGL(kern, dim3(chunks, nimg), dim3(nt), 0, st, z, nimg, plane_px, part, chunk_vec);
-  };
-  const bool u8x = big && hv && hv[2] && hv[3] == 'u';
-  if (big && m == 'h') go(latent_hist_kernel<32, false, 1024>, 1024);
-  else if (big && m == 'g') u8x ? go(latent_hist_kernel<16, false, 1024, 8>, 1024) : go(latent_hist_kernel<16, false, 1024>, 1024);
-  else if (big && m == '4') go(latent_hist_kernel<4, false, 1024>, 1024);
-  else if (big) u8x ? go(latent_hist_kernel<8, false, 1024, 8>, 1024) : go(latent_hist_kernel<8, false, 1024>, 1024);
-  else if (m == '1') zb ? go(latent_hist_kernel<1, true, 256>, 256) : go(latent_hist_kernel<1, false, 256>, 256);
-  else if (m == '8') zb ? go(latent_hist_kernel<8, true, 256>, 256) : go(latent_hist_kernel<8, false, 256>, 256);
-  else zb ? go(latent_hist_kernel<4, true, 256>, 256) : go(latent_hist_kernel<4, false, 256>, 256);
+  const int chunks = hist_chunks(nimg, plane_px, &chunk_vec, big ? 512 : 1536);
+  if (big)
+    hipLaunchKernelGGL((latent_hist_kernel<16, false, 1024>), dim3(chunks, nimg), dim3(1024), 0, st, z, nimg, plane_px, part,
+                       chunk_vec);
+  else
+    hipLaunchKernelGGL((latent_hist_kernel<8, false, 256>), dim3(chunks, nimg), dim3(256), 0, st, z, nimg, plane_px, part,
+                       chunk_vec);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hist_entropy_kernel, dim3(3 * nimg), dim3(1024), 0, st, part, chunks, (float)plane_px * 32.0f,

@@ -380,11 +380,11 @@ def skewed_latent():
     return z, O.histograms(z), O.hist_entropy(z).ravel()
 
 
-@pytest.mark.parametrize("variant", [None, "8", "8z", "1", "4", "8b1", "8b2u", "4b2", "gb1", "gb2u", "hb1"])
+@pytest.mark.parametrize("variant", [None, "big", "small"])
 def test_entropy_kernel_variants_count_exactly(codecs, skewed_latent, monkeypatch, variant):
-    """Every histogram kernel behind launch_hist's NIC_HIST A/B switch (256- and 1024-thread
-    blocks, 1-32 LDS replicas, zero-bin skipping, 4 or 8 loads in flight) against the oracle;
-    None = the library default."""
+    """Both histogram kernels launch_hist picks by latent size (1024-thread blocks with 16 LDS
+    replicas, 256-thread blocks with 8), forced on the same latent by NIC_HIST, against the
+    oracle; None = the library's choice."""
     z, counts, bits_ref = skewed_latent
     if variant is None:
         monkeypatch.delenv("NIC_HIST", raising=False)
@@ -690,26 +690,17 @@ def _alt_child(tmp_path, switches, tag):
     return dump
 
 
-@pytest.mark.parametrize("switches", [{"NIC_WS": "0", "NIC_D8": "tile"}, {"NIC_D8": "strip"}, {"NIC_D8G": "l"},
-                                      {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"}, {"NIC_K3P_BAL": "0"},
-                                      {"NIC_D1": "x"}, {"NIC_D1": "p"}],
-                         ids=["ws0-tile", "strip", "gather-lds", "k3-unfused", "k3-lockstep", "k3-equal-rows",
-                              "dconv1-tile", "dconv1-perphase"])
+@pytest.mark.parametrize("switches", [{"NIC_K3P": "0"}], ids=["k3-unfused"])
 def test_alternative_kernels_parity(tmp_path, switches, weights_spread):
-    """The one-tile-per-block split-f16 convs, standalone conv1 and tile dconv8 (NIC_WS=0,
-    NIC_D8=tile), the strip-walk dconv8 behind an unfused dconv7 (NIC_D8=strip), the k3 layers
-    as two launches (NIC_K3P=0) or the fused pair in lockstep order, the per-phase dconv1
-    walk (NIC_D1=p), the fused pair's equal-rows block ranges (NIC_K3P_BAL=0) ... meet the
-    golden contract too; they run in a child process because the switches are read when the
-    library loads."""
+    """The k3 residual layers as two weight-stationary launches (NIC_K3P=0: the form planes
+    the fused pair does not take run, e.g. config 4's 192 columns) meet the golden contract
+    and are bit-identical to the fused pair; child process (the switch is read when the
+    library loads).  The other kernel forms of rounds 1-5 were measured slower and removed."""
     dump = _alt_child(tmp_path, switches, "v")
-    if switches in ({"NIC_D8G": "l"}, {"NIC_D1": "p"}, {"NIC_K3P": "0"}, {"NIC_K3P_SK": "0"},
-                    {"NIC_K3P_BAL": "0"}):
-        # the LDS-staged gather sums the same projections in the same order as the direct one;
-        # the default all-phase dconv1 runs the per-phase walk's MFMA chains and epilogue; the
-        # default (direct 9-tap) fused k3 residual pair runs the same chains and epilogues as
-        # the two weight-stationary launches, in either step order and under either block range
-        # split (a range boundary inside a plane recomputes the same conv_a row): bit-identical
+    if switches == {"NIC_K3P": "0"}:
+        # the fused k3 residual pair runs the same MFMA chains and epilogues as the two
+        # weight-stationary launches (a block range boundary inside a plane recomputes the
+        # same conv_a row): bit-identical
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from alt_kernels_check import alt_cases
 

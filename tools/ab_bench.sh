@@ -2,7 +2,7 @@
 # Same-box A/B of library builds: bench.py with NIC_LIB pointing at each build in turn,
 # ROUNDS interleaved passes (box-to-box variance exceeds most kernel deltas).
 # usage: VARIANTS="cur=neural_network_image_compression_amd/libnic.so r1k=ab/libnic_r1k.so" bash tools/ab_bench.sh TAG
-# a variant may add env settings after commas: "tile=neural_network_image_compression_amd/libnic.so,NIC_WS=0"
+# a variant may add env settings after commas: "unfused=neural_network_image_compression_amd/libnic.so,NIC_K3P=0"
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

@@ -37,9 +37,11 @@ int main() {
   CK(hipMalloc(&out, (size_t)P * OH * OW * 64 * 4));
   // random f16 weights in [-0.05, 0.05] (constant patterns draw less MFMA power: the clock,
   // and so the cycle split, would not be the real kernel's)
-  auto rnd16 = [](size_t n) {
+  // C12_ZERO=1: all-zero weights (the schedule's clock, not the power budget's)
+  const bool zero = getenv("C12_ZERO") && getenv("C12_ZERO")[0] == '1';
+  auto rnd16 = [zero](size_t n) {
     std::vector<_Float16> h(n);
-    for (auto& v : h) v = (_Float16)((rand() % 2000) / 20000.f - 0.05f);
+    for (auto& v : h) v = zero ? (_Float16)0.f : (_Float16)((rand() % 2000) / 20000.f - 0.05f);
     return h;
   };
   CK(hipMalloc(&wx, (size_t)2 * 25 * 32 * 64 * 4));
@@ -98,7 +100,11 @@ int main() {
   ms /= iters;
   std::vector<unsigned long long> hs((size_t)maxb * 64);
   CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
+#if NIC_C12R  // c12r_wave: wave 0 = R2 (stream), wave 4 = R1 (vector work)
+  const char* nm[7] = {"top-bar", "acc+dma+epi", "flag+acc-st", "conv1", "dma-wait", "stream", "other"};
+#else
   const char* nm[7] = {"top-bar", "epi|patch", "flag-wait", "(part+)conv1", "rgb-issue", "stream", "other"};
+#endif
   printf("conv12 %.4f ms (%.0f TFLOP/s)\n", ms, 85.564 / ms);
 #ifdef NIC_STAMPS
   for (int w = 0; w < 8; w += 4) {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of env-var variants of one build, alternating on one box: each argument is
-# NAME=VALUE (or "base" for no setting), e.g. TAG=x bash tools/env_ab.sh base NIC_D7_STAG=2
+# NAME=VALUE (or "base" for no setting), e.g. TAG=x bash tools/env_ab.sh base NIC_K3P=0
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-r5j}

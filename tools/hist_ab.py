@@ -21,7 +21,7 @@ x = torch.randint(0, 256, (F, 2160, 3840, 3), generator=g, dtype=torch.uint8).cu
 z = c.encode(x)
 torch.cuda.synchronize()
 ref = None
-for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "4", "8", "8z"]):
+for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["d", "big", "small"]):
     if v == "d":  # the library default
         os.environ.pop("NIC_HIST", None)
     else:

@@ -1,6 +1,6 @@
 """Host-array surface (Encoder()(numpy) -> Decoder()(numpy), config-2 batch) per chunk plan and
 staging-copy thread count, each setting in a fresh process (the switches are read at library
-load): NIC_HOST_EDGE (edge-chunk weight, permille of a middle chunk), chunks, and
+load): chunks and
 NIC_HOST_COPY_THREADS.  Prints one JSON line per setting; usage: python tools/host_plan_sweep.py [n settings]"""
 import json
 import os
@@ -34,13 +34,8 @@ r["ratio"] = r["device_ms"] / r["roundtrip_ms"]
 print(json.dumps({k: round(v, 4) for k, v in r.items()}))
 ''' % ROOT
 
-SETTINGS = [("3", {}), ("3", {"NIC_HOST_COPY_THREADS": "0"}), ("3", {"NIC_HOST_EDGE": "250"}),
-            ("3", {"NIC_HOST_EDGE": "350"}), ("4", {"NIC_HOST_EDGE": "300"}), ("4", {}), ("2", {}),
-            ("5", {"NIC_HOST_EDGE": "300"})]
-
-if len(sys.argv) > 1 and sys.argv[1] == "k3bal":  # step-balanced k3 pair ranges vs equal rows, 3 alternating rounds
-    SETTINGS = [("3", {}), ("3", {"NIC_K3P_BAL": "0"})] * 3
-    sys.argv[1:] = []
+SETTINGS = [("3", {}), ("3", {"NIC_HOST_COPY_THREADS": "0"}), ("3", {"NIC_HOST_COPY_THREADS": "7"}), ("4", {}),
+            ("2", {}), ("5", {})]
 for chunks, env in SETTINGS[:int(sys.argv[1]) if len(sys.argv) > 1 else None]:
     e = dict(os.environ, **env)
     out = subprocess.run([sys.executable, "-c", CHILD, chunks], env=e, capture_output=True, text=True, timeout=240)

@@ -8,7 +8,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 B="--no-cpu-baseline --no-host-path --no-quality --no-power-probe --no-parity"
 show() {
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], ' '.join(f\"{k}={v['avg_ms']:.4f}\" for k,v in d['layers'].items()))" "$1" "$2"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], ' '.join(f\"{k}={v['avg_ms']:.4f}\" for k,v in d['layers'].items() if 'avg_ms' in v))" "$1" "$2"
 }
 for r in 1 2 3; do
   for v in "$@"; do
