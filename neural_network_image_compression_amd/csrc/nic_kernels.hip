@@ -2592,6 +2592,9 @@ __global__ __launch_bounds__(512, 1) void conv_k3pair_kernel(ConvArgs a, K3Range
 
 // strips for a plane of W columns (0: the fused pair does not take it): one for W <= 64, else
 // 62-column strips when their lanes waste at most 10 % (4K frames: 16 strips over 960 columns)
+// (Config 4's 192-column planes would take 4 strips with 23 % of the lanes idle: the pair then
+// takes 0.72 / 0.70 ms against 0.31 + 0.35 / 0.30 + 0.34 ms for the two launches, step 3.18 vs
+// 3.14 ms on one box, 3 rounds -- so those planes keep the two launches)
 static int k3pair_strips(int W) {
   if (W <= K3P_MAX_W) return 1;
   const int n = (W + K3P_SW - 1) / K3P_SW;

@@ -14,11 +14,12 @@ for r in 1 2 3; do
   for v in "$@"; do
     lib=$PWD/neural_network_image_compression_amd/libnic_$v.so
     [ "$v" = base ] && lib=$PWD/neural_network_image_compression_amd/libnic.so
-    NIC_LIB=$lib timeout -k 10 180 python bench.py --steps 30 --warmup 20 $B > $O/${v}_$r.json 2> $O/${v}_$r.err
+    NIC_LIB=$lib timeout -k 10 180 python bench.py --workload ${WL:-config2} --steps 30 --warmup 20 $B > $O/${v}_$r.json 2> $O/${v}_$r.err
     rc=$?; [ $rc -eq 0 ] || { echo "$v rc=$rc"; tail -5 $O/${v}_$r.err; exit $rc; }
     show $O/${v}_$r.json "$v/$r"
   done
 done
+[ "${NO4K:-0}" = 1 ] && exit 0
 for v in "$@"; do
   lib=$PWD/neural_network_image_compression_amd/libnic_$v.so
   [ "$v" = base ] && lib=$PWD/neural_network_image_compression_amd/libnic.so
