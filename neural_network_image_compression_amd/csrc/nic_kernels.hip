@@ -1205,6 +1205,10 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   constexpr int T0 = 25 * TS / NTS, T1 = 25 * (TS + 1) / NTS, NT = T1 - T0;
   using G = GeomS2<CIN, TH, TW>;
   constexpr int TAP_BYTES = CIN * COUT * 4;
+  // every wave issues its share of the halo DMA pieces.  Round-6 A/B (profiles/r6_ab_logs.txt
+  // r6o): leaving the ts = 0 waves (which carry the epilogue) out of the issue moves their
+  // 1,400 cycles of pieces into the other tap groups' chains; the tile period stays ~4,600
+  // cycles and conv8 is 1 % slower, so the pieces stay spread over all waves
   constexpr int NPP = (G::NPIECE + NW - 1) / NW;
   constexpr int PART = MT * 1024;  // one wave's partial tile: MT x 64 lanes x 16 B
   char* part = lds + 2 * G::HALO_BYTES;  // [parity][NTS-1][NCG] partial tiles
@@ -1361,9 +1365,10 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
   } while (0)
 #endif
   for (int i = 0; i <= ntile; ++i) {
-    WS2_MARK(6);  // conv2 MFMAs + partials (previous iteration)
+    WS2_MARK(6);  // (the previous iteration's tail)
     dma_wait_all();
     lds_reads_done();
+    WS2_MARK(5);      // DMA / LDS drain
     stage_barrier();  // halo of tile i complete; partials of tile i-1 written
     WS2_MARK(0);      // top barrier
     if constexpr (TS == 0) {
@@ -1406,8 +1411,13 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
         }
       }
     }
+    WS2_MARK(1);  // epilogue (ts 0)
     if (i == ntile) break;
-    if (i + 1 < ntile) issue(i + 1);  // into the buffer of tile i-1
+    // the next tile's halo into the buffer of tile i-1.  (Its pieces spread through the MFMA
+    // stream below instead, one per 2 / 3 groups, took conv8 from 0.0635 to 0.0665 / 0.0701 ms:
+    // a piece waiting for the texture path stalls the in-order wave's MFMAs behind it.)
+    if (i + 1 < ntile) issue(i + 1);
+    WS2_MARK(2);  // halo DMA issue
     if constexpr (HIST) {
       h2_p = h1_p;
       h2_y = h1_y;
@@ -1453,11 +1463,13 @@ __device__ __forceinline__ void ws2_wave(const ConvArgs& a, char* lds, int model
       __builtin_amdgcn_sched_barrier(0);  // keep the stream order
     });
     if constexpr (NIC_WS2_PRIO && !HIST) __builtin_amdgcn_s_setprio(0);
+    WS2_MARK(3);  // MFMA stream
     if constexpr (TS > 0) {  // partial sums of tile i for the ts = 0 wave of this cg
       char* pp = part + (((i & 1) * (NTS - 1) + TS - 1) * NCG + cg) * PART + lane * 16;
 #pragma unroll
       for (int m = 0; m < MT; ++m) *(f32x4*)(pp + m * 1024) = acc[m];
     }
+    WS2_MARK(4);  // partials
     // HIST: the ts = 1 waves count after their own MFMA stream, where they would wait at the
     // next barrier: tile i-2's codes (stored by ts = 0 at the top of iteration i-1)
     if constexpr (HIST && TS == 1) {

@@ -36,7 +36,7 @@ int main() {
   auto hin = rnd16((size_t)P * H * W * 64 * 2, 0.5f);
   CK(hipMemcpy(in, hin.data(), hin.size() * 2, hipMemcpyHostToDevice));
   CK(hipMalloc(&wx, (size_t)2 * 25 * 64 * 32 * 4));
-  auto hw = rnd16((size_t)2 * 25 * 64 * 32 * 2, 0.05f);
+  auto hw = rnd16((size_t)2 * 25 * 64 * 32 * 2, getenv("C8_ZERO") ? 0.f : 0.05f);  // C8_ZERO: all-zero weights
   CK(hipMemcpy(wx, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
   CK(hipMalloc(&lat, (size_t)N * OH * OW * 96));
   CK(hipMalloc(&bias, 2 * 32 * 4));
@@ -77,17 +77,18 @@ int main() {
   std::vector<unsigned long long> hs((size_t)maxb * 64);
   CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
   printf("conv8 %.4f ms (%.0f TFLOP/s)\n", ms, 20.133 / ms);
+  const char* nm[7] = {"top-bar", "epilogue", "dma-issue", "stream", "partials", "drain", "tail"};
   for (int w = 0; w < 8; ++w) {
-    double top = 0, rest = 0, nt = 0;
+    double sum[7] = {}, nt = 0;
     for (int b = 0; b < 256; ++b) {
       const unsigned long long* o = &hs[((size_t)b * 8 + w) * 8];
       if (o[7] == 0) continue;
-      top += o[0];
-      rest += o[6];
+      for (int q = 0; q < 7; ++q) sum[q] += o[q];
       nt += o[7];
     }
-    printf("  wave %d (cg %d, ts %d) per tile: top-barrier %5.0f  work %5.0f cycles  (%.1f tiles/block)\n", w, w % 2,
-           w / 2, top / nt, rest / nt, nt / 256);
+    printf("  wave %d (cg %d, ts %d) per tile:", w, w % 2, w / 2);
+    for (int q = 0; q < 7; ++q) printf(" %s %5.0f", nm[q], sum[q] / nt);
+    printf("  (%.1f tiles/block)\n", nt / 256);
   }
   return 0;
 }
