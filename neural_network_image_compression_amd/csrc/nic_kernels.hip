@@ -1659,6 +1659,9 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
 // so the LDS flag orders its reuse.  Different summation order from the tap-split form (one
 // 75-MFMA chain per output instead of two 36 / 39 chains added in fp32): a different fp32
 // rounding of the same sums, within the oracle contract.
+#ifndef NIC_C12_REUSE
+#define NIC_C12_REUSE 1  // 0 (A/B build): tiles bi, bi + nb, ... and every conv1 halo computed in full
+#endif
 template <int ROLE>
 __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int model, int bi, int nb) {
   constexpr int CIN = 32, COUT = 64, MT = 4, NCG = 4;
@@ -1674,7 +1677,14 @@ __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int mode
   const int per_plane = a.tiles_y * a.tiles_x;
   const int p0 = model ? a.nimg : 0, np = model ? a.P - a.nimg : a.nimg;
   const int ntot = np * per_plane;
-  const int ntile = bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  // the block's tiles: a contiguous raster range (its successive tiles are row neighbours, so
+  // conv1's halo columns shared with the previous tile are copied, not recomputed).  Same box
+  // (profiles/r6_ab_logs.txt r6r): 4K conv12 3.397 -> 3.333 ms, config 2 equal (its rows are 8
+  // tiles); the contiguous walk alone 3.414
+  constexpr bool CONTIG = NIC_C12_REUSE != 0;
+  const int t_first = CONTIG ? (int)((long long)bi * ntot / nb) : bi;
+  const int ntile = CONTIG ? (int)((long long)(bi + 1) * ntot / nb) - t_first : bi < ntot ? (ntot - bi + nb - 1) / nb : 0;
+  const int t_step = CONTIG ? 1 : nb;
   float rmax = 0.f;
   if (threadIdx.x < NCG) pflag[threadIdx.x] = 0;
 #ifdef NIC_STAMPS  // per wave cycle sums (tools/c12_stamps.cpp)
@@ -1760,7 +1770,7 @@ __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int mode
   } else {
     __builtin_amdgcn_s_setprio(1);  // the vector wave's MFMAs and VALU ahead of the bare stream
     TileWalk w_patch, w_c1, w_ep;
-    w_patch.init(bi, nb, a.tiles_y, a.tiles_x);
+    w_patch.init(t_first, t_step, a.tiles_y, a.tiles_x);
     w_c1 = w_ep = w_patch;
     auto tile_take = [&](TileWalk& w, int& p, int& t0y, int& t0x) {
       int pl, ty, tx;
@@ -1799,22 +1809,45 @@ __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int mode
       tile_take(w_patch, p, t0y, t0x);
       pdma.issue(a, cg, p, t0y, t0x, patches + (i & 1) * 2 * C12_PLANE);
     };
-    // conv1 of tile i on this wave's pixel tiles cg + 4u of the 19 x 19 halo (patch buffer
-    // i & 1 -> halo buffer i & 1), software-pipelined: all fragment reads, then the MFMA chains,
-    // then the epilogues
-    auto conv1 = [&](int i) {
-      constexpr int NPT = (G::HH * G::HW + 15) / 16, PTW = (NPT + 3) / 4;
-      int p, t0y, t0x;
-      tile_take(w_c1, p, t0y, t0x);
+    // conv1 of tile i on this wave's pixel tiles cg + 4u (patch buffer i & 1 -> halo buffer
+    // i & 1), software-pipelined: all fragment reads, then the MFMA chains, then the epilogues.
+    // Full: the 19 x 19 halo in 23 pixel tiles of 16 (raster order).  REUSE (tile i-1 is the left
+    // neighbour): halo columns 0-2 are columns 16-18 of tile i-1's halo (buffer (i-1) & 1, which
+    // R2 only reads now), copied; conv1 computes columns 3-18, one halo row per pixel tile (19).
+    auto conv1_tiles = [&](auto reuse_c, int i, int t0y, int t0x) {
+      constexpr bool REUSE = decltype(reuse_c)::value;
+      constexpr int NPT = REUSE ? G::HH : (G::HH * G::HW + 15) / 16, PTW = (NPT + 3) / 4;
       char* halo = lds + (i & 1) * G::HALO_BYTES;
       const char* ph = patches + (i & 1) * 2 * C12_PLANE;
       const int c1y0 = 2 * t0y - a.pad_y, c1x0 = 2 * t0x - a.pad_x;
+      if constexpr (REUSE) {  // 19 rows x 3 records x 8 16-B chunks over the 4 R1 waves
+        const char* prev = lds + ((i - 1) & 1) * G::HALO_BYTES;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int c = (cg + 4 * k) * 64 + lane;
+          if (c < G::HH * 3 * 8) {
+            const int rec = c >> 3, ch = c & 7, hy = rec / 3, j = rec - hy * 3;
+            const u32x4 v = *(const u32x4*)(prev + hy * G::RPB + G::col(16 + j) * G::PSB + ch * 16);
+            *(u32x4*)(halo + hy * G::RPB + G::col(j) * G::PSB + ch * 16) = v;
+          }
+        }
+      }
+      auto pix = [&](int pt, int& hy, int& hx) {  // pixel tile pt, lane l16 -> halo (hy, hx)
+        if constexpr (REUSE) {
+          hy = pt;
+          hx = 3 + l16;
+        } else {
+          const int q = 16 * pt + l16;
+          hy = q / G::HW;
+          hx = q - hy * G::HW;
+        }
+      };
       f16x8 bh[PTW], bl[PTW];
 #pragma unroll
       for (int u = 0; u < PTW; ++u) {
-        const int q = 16 * (cg + 4 * u) + l16;
-        const int qq = q < G::HH * G::HW ? q : 0;
-        const int hy = qq / G::HW, hx = qq - hy * G::HW;
+        int hy, hx;
+        pix(cg + 4 * u, hy, hx);
+        if (hy >= G::HH) hy = hx = 0;  // past the last pixel tile (not stored)
         const char* pb = ph + (2 * hy * C12_PPW + hx) * 4;
         u32x4 H, L;
 #pragma unroll
@@ -1838,9 +1871,9 @@ __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int mode
       for (int u = 0; u < PTW; ++u) {
         const int pt = cg + 4 * u;
         if (pt >= NPT) break;  // wave-uniform
-        const int q = 16 * pt + l16;
-        const bool qv = q < G::HH * G::HW;
-        const int hy = qv ? q / G::HW : 0, hx = qv ? q - hy * G::HW : 0;
+        int hy, hx;
+        pix(pt, hy, hx);
+        const bool qv = hy < G::HH;
         const bool in1 = qv && (unsigned)(c1y0 + hy) < (unsigned)a.H && (unsigned)(c1x0 + hx) < (unsigned)a.W;
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
@@ -1855,6 +1888,14 @@ __device__ __forceinline__ void c12r_wave(const ConvArgs& a, char* lds, int mode
             *(u32x4*)(halo + hy * G::RPB + G::col(hx) * G::PSB + (g & 1) * CIN * 2 + (16 * ct + 4 * (g & ~1)) * 2) = q16;
         }
       }
+    };
+    auto conv1 = [&](int i) {
+      int p, t0y, t0x;
+      tile_take(w_c1, p, t0y, t0x);
+      if (CONTIG && i > 0 && t0x > 0)
+        conv1_tiles(std::integral_constant<bool, true>{}, i, t0y, t0x);
+      else
+        conv1_tiles(std::integral_constant<bool, false>{}, i, t0y, t0x);
     };
     const int st_off = (g & 1) * COUT + cg * 16 + 8 * (g >> 1);  // split store granule (swap16_pair)
     // prologue: patches 0, 1 -> barrier -> conv1(0) -> barrier
