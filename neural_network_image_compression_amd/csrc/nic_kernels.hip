@@ -819,12 +819,6 @@ struct GeomWS {
 #define NIC_RES_DMA 1
 #endif
 constexpr bool kResDma = NIC_RES_DMA != 0;
-// diagnostic build only: no projection MFMAs / stores in dconv7 (wrong results)
-#ifdef NIC_DIAG_NOPROJ
-constexpr bool kProjOff = true;
-#else
-constexpr bool kProjOff = false;
-#endif
 template <int CIN, int COUT, int TH, int TW, bool RESID, int KH, int KW, bool TRP, bool PROJ = false>
 __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model, int bi, int nb, int tb, int py,
                                         int px, bool copy_w8 = true) {
@@ -1017,9 +1011,6 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int y = ep_y + 2 * m + (l16 >> 3), x = ep_x + (l16 & 7);
-#ifdef NIC_DIAG_NOEPI  // diagnostic build only: no epilogue arithmetic (wrong results)
-        u32x4 q = __builtin_bit_cast(u32x4, acc[m]);
-#else
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = leaky02(scale_bias(acc[m][r], scale, bias[r]));
@@ -1038,7 +1029,6 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         f16x4 hi, lo;
         split4(v, hi, lo);
         u32x4 q = swap16_pair(hi, lo);  // even g: hi of 8 channels, odd g: lo of the same 8
-#endif
         if constexpr (PROJ) {  // chunk (g & 1) * 8 + 2w + g / 2 of pixel 16m + l16
           const int pp = 16 * m + l16, ch = (g & 1) * 8 + 2 * wave + (g >> 1);
           *(u32x4*)(hproj + pp * 256 + ((ch ^ (pp & 15)) << 4)) = q;
@@ -1055,13 +1045,11 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
     if constexpr (PROJ)
       if (i > 0) {
         lds_reads_done();  // lgkmcnt(0): this wave's hproj writes have landed
-#ifndef NIC_DIAG_NOBAR2  // diagnostic build: no projection barrier (racy, wrong results)
         stage_barrier();   // the whole tile's channels are in hproj
-#endif
       }
     if constexpr (!PROJ)
       if (i + 1 < ntile) issue(i + 1);  // into the buffer tile i-1 used
-    if constexpr (PROJ && !kProjOff)
+    if constexpr (PROJ)
       if (i > 0) {  // tile i-1's projection (4 chunks of 3 MFMAs) and its stores
         proj_load_a(0);
         proj_load_w(0);
@@ -1127,12 +1115,10 @@ __device__ __forceinline__ void ws_body(const ConvArgs& a, char* lds, int model,
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][1], fb[m][0], acc[m], 0, 0, 0);  // w_lo*a_hi
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][1], acc[m], 0, 0, 0);  // w_hi*a_lo
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[t][ks][0], fb[m][0], acc[m], 0, 0, 0);  // w_hi*a_hi
-#ifndef NIC_DIAG_NOLDS  // diagnostic build: the fragments of step 0 reused (wrong results)
         if (st + 1 < NSTEP) {
           fb[m][0] = frag(m, st + 1, 0);
           fb[m][1] = frag(m, st + 1, 1);
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);  // keep the rolling order (no hoisted reads)
       }
     }

@@ -3,7 +3,7 @@
 // data, timed with hipEvents after 30 warm-up launches.  Built in variants with the
 // NIC_DIAG_* switches of nic_kernels.hip (each removes one part of the work and gives wrong
 // results) to bound what each part costs; with -DNIC_STAMPS it prints the per-tile cycle split.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off [-DNIC_DIAG_NOEPI ...] \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off [-DNIC_DIAG_ONETILE ...] \
 //     tools/d7_diag.cpp -o ab/d7_base
 #include "../neural_network_image_compression_amd/csrc/nic_kernels.hip"
 
