@@ -238,6 +238,15 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
  *     bias nullable; x_scale / w_scale nullable device floats (power-of-two operand scales from
  *     nic_absmax_scale, undone exactly in the epilogue).  work: 16-B aligned device scratch of
  *     nic_conv_gather_work() bytes (the split weights).  cin, cout <= 64.
+ * nic_conv_gather_act: the same with act = 1 applying the layers' activation in the epilogue,
+ *     y = leaky_relu(bias + sum, 0.2) (Keras Conv2D(..., activation=tf.nn.leaky_relu),
+ *     encoder.py:10-17 / decoder.py:10-17); act = 0 is nic_conv_gather.
+ * nic_act_bias_grad: the backward of that epilogue over a (rows, cols) NHWC tensor (rows = n h w):
+ *     dz = dy * (act && !(y > 0) ? 0.2 : 1) (tf.nn.leaky_relu's gradient, from the layer's output
+ *     y), db[c] = sum over rows of dz[row][c] (BiasAddGrad) and dz_scale[0] = nic_absmax_scale
+ *     of dz, from one pass; any output may be NULL (not all; act = 0 and dz NULL: dz is dy).
+ *     Deterministic (per-block column sums in `work`, added in block order); work must hold
+ *     nic_act_bias_grad_work() floats.  cols <= 64.
  * nic_conv_wgrad: dw[ky][kx][a][b'] = sum over b, u of
  *     gat[b][stride*uy+ky-pad_y][stride*ux+kx-pad_x][a] * dir[b][uy][ux][b']
  *     (Conv2D: gat = x, dir = dy, dw HWIO; Conv2DTranspose: gat = dy, dir = x, dw HWOI);
@@ -258,6 +267,13 @@ int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* w
                     int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
                     const float* w_scale, float* y, int oh, int ow, int cout, void* work, int64_t work_bytes,
                     void* stream);
+int nic_conv_gather_act(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
+                        int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                        const float* w_scale, float* y, int oh, int ow, int cout, int act, void* work,
+                        int64_t work_bytes, void* stream);
+int nic_act_bias_grad_work(int64_t rows, int cols, int64_t* floats);
+int nic_act_bias_grad(const float* y, const float* dy, int64_t rows, int cols, int act, float* dz, float* db,
+                      float* dz_scale, float* work, int64_t work_floats, void* stream);
 int nic_conv_wgrad_work(int n, int uh, int uw, int kh, int kw, int ca, int cb, int64_t* floats);
 int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb, int kh,
                    int kw, int stride, int pad_y, int pad_x, const float* gat_scale, const float* dir_scale, float* dw,

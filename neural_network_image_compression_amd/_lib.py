@@ -82,6 +82,11 @@ _SIGNATURES = {
     "nic_conv_gather_work": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_int64)]),
     "nic_conv_gather": (ctypes.c_int, [c_vp] + [ctypes.c_int] * 4 + [c_vp] + [ctypes.c_int] * 7 + [c_vp] * 4
                         + [ctypes.c_int] * 3 + [c_vp, ctypes.c_int64, c_vp]),
+    "nic_conv_gather_act": (ctypes.c_int, [c_vp] + [ctypes.c_int] * 4 + [c_vp] + [ctypes.c_int] * 7 + [c_vp] * 4
+                            + [ctypes.c_int] * 4 + [c_vp, ctypes.c_int64, c_vp]),
+    "nic_act_bias_grad_work": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+    "nic_act_bias_grad": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp,
+                                         c_vp, ctypes.c_int64, c_vp]),
     "nic_conv_wgrad_work": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_int64)]),
     "nic_conv_wgrad": (ctypes.c_int, [c_vp] + [ctypes.c_int] * 4 + [c_vp] + [ctypes.c_int] * 8 + [c_vp] * 4
                        + [ctypes.c_int64, c_vp]),

@@ -1383,24 +1383,61 @@ int nic_conv_gather_work(int kh, int kw, int cin, int cout, int64_t* bytes) {
   return NIC_OK;
 }
 
+static int conv_gather_impl(const char* name, const float* x, int n, int h, int w, int cin, const float* wt, int kh,
+                            int kw, int wt_layout, int stride, int pad_y, int pad_x, int transposed, const float* bias,
+                            const float* x_scale, const float* w_scale, float* y, int oh, int ow, int cout, int act,
+                            void* work, int64_t work_bytes, void* stream) {
+  if (n < 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
+      !train_dims_ok(cin) || !train_dims_ok(cout) || pad_y < 0 || pad_x < 0)
+    return fail(NIC_ESHAPE, "%s: bad shape n=%d %dx%dx%d -> %dx%dx%d k=%dx%d s=%d pad=%d,%d", name, n, h, w, cin, oh, ow,
+                cout, kh, kw, stride, pad_y, pad_x);
+  if ((wt_layout != 0 && wt_layout != 1) || (transposed != 0 && transposed != 1) || (act != 0 && act != 1))
+    return fail(NIC_EINVAL, "%s: wt_layout / transposed / act must be 0 or 1", name);
+  if (n == 0) return NIC_OK;
+  if (!x || !wt || !y || !work) return fail(NIC_EINVAL, "%s: NULL argument", name);
+  const int64_t need = (int64_t)train_gather_work_bytes(kh, kw, cin, cout);
+  if (work_bytes < need)
+    return fail(NIC_EINVAL, "%s: work holds %lld bytes, needs %lld", name, (long long)work_bytes, (long long)need);
+  if (((uintptr_t)work & 15) != 0) return fail(NIC_EINVAL, "%s: work must be 16-byte aligned", name);
+  HIP_TRY(launch_conv_gather(x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed, bias, x_scale,
+                             w_scale, y, oh, ow, cout, act, work, (hipStream_t)stream));
+  return NIC_OK;
+}
+
 int nic_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
                     int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
                     const float* w_scale, float* y, int oh, int ow, int cout, void* work, int64_t work_bytes,
                     void* stream) {
-  if (n < 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || kh <= 0 || kw <= 0 || kh * kw > 64 || stride <= 0 ||
-      !train_dims_ok(cin) || !train_dims_ok(cout) || pad_y < 0 || pad_x < 0)
-    return fail(NIC_ESHAPE, "nic_conv_gather: bad shape n=%d %dx%dx%d -> %dx%dx%d k=%dx%d s=%d pad=%d,%d", n, h, w, cin,
-                oh, ow, cout, kh, kw, stride, pad_y, pad_x);
-  if ((wt_layout != 0 && wt_layout != 1) || (transposed != 0 && transposed != 1))
-    return fail(NIC_EINVAL, "nic_conv_gather: wt_layout / transposed must be 0 or 1");
-  if (n == 0) return NIC_OK;
-  if (!x || !wt || !y || !work) return fail(NIC_EINVAL, "nic_conv_gather: NULL argument");
-  const int64_t need = (int64_t)train_gather_work_bytes(kh, kw, cin, cout);
-  if (work_bytes < need)
-    return fail(NIC_EINVAL, "nic_conv_gather: work holds %lld bytes, needs %lld", (long long)work_bytes, (long long)need);
-  if (((uintptr_t)work & 15) != 0) return fail(NIC_EINVAL, "nic_conv_gather: work must be 16-byte aligned");
-  HIP_TRY(launch_conv_gather(x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed, bias, x_scale,
-                             w_scale, y, oh, ow, cout, work, (hipStream_t)stream));
+  return conv_gather_impl("nic_conv_gather", x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x, transposed,
+                          bias, x_scale, w_scale, y, oh, ow, cout, 0, work, work_bytes, stream);
+}
+
+int nic_conv_gather_act(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int wt_layout,
+                        int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
+                        const float* w_scale, float* y, int oh, int ow, int cout, int act, void* work,
+                        int64_t work_bytes, void* stream) {
+  return conv_gather_impl("nic_conv_gather_act", x, n, h, w, cin, wt, kh, kw, wt_layout, stride, pad_y, pad_x,
+                          transposed, bias, x_scale, w_scale, y, oh, ow, cout, act, work, work_bytes, stream);
+}
+
+int nic_act_bias_grad_work(int64_t rows, int cols, int64_t* floats) {
+  if (!floats) return fail(NIC_EINVAL, "nic_act_bias_grad_work: NULL argument");
+  if (rows < 0 || !train_dims_ok(cols)) return fail(NIC_ESHAPE, "nic_act_bias_grad_work: bad shape");
+  *floats = (int64_t)train_abg_work_floats(rows, cols);
+  return NIC_OK;
+}
+
+int nic_act_bias_grad(const float* y, const float* dy, int64_t rows, int cols, int act, float* dz, float* db,
+                      float* dz_scale, float* work, int64_t work_floats, void* stream) {
+  if (rows < 0 || !train_dims_ok(cols) || rows > (int64_t)INT32_MAX * 256)
+    return fail(NIC_ESHAPE, "nic_act_bias_grad: bad shape rows=%lld cols=%d", (long long)rows, cols);
+  if (act != 0 && act != 1) return fail(NIC_EINVAL, "nic_act_bias_grad: act must be 0 or 1");
+  if (!dz && !db && !dz_scale) return fail(NIC_EINVAL, "nic_act_bias_grad: no output requested");
+  if (rows > 0 && (!dy || (act && !y))) return fail(NIC_EINVAL, "nic_act_bias_grad: NULL argument");
+  if (!work || work_floats < (int64_t)train_abg_work_floats(rows, cols))
+    return fail(NIC_EINVAL, "nic_act_bias_grad: work holds %lld floats, needs %lld", (long long)work_floats,
+                (long long)train_abg_work_floats(rows, cols));
+  HIP_TRY(launch_act_bias_grad(y, dy, rows, cols, act, dz, db, dz_scale, work, (hipStream_t)stream));
   return NIC_OK;
 }
 

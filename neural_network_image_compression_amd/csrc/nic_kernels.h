@@ -208,7 +208,10 @@ size_t train_gather_work_bytes(int kh, int kw, int cin, int cout);
 hipError_t launch_absmax_scale(const float* x, long long n, float* scale, float* work, hipStream_t st);
 hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int layout,
                               int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
-                              const float* w_scale, float* y, int oh, int ow, int cout, void* work, hipStream_t st);
+                              const float* w_scale, float* y, int oh, int ow, int cout, int act, void* work, hipStream_t st);
+size_t train_abg_work_floats(long long rows, int cols);
+hipError_t launch_act_bias_grad(const float* y, const float* dy, long long rows, int cols, int act, float* dz, float* db,
+                                float* dz_scale, float* work, hipStream_t st);
 hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float* dir, int uh, int uw, int cb,
                              int kh, int kw, int stride, int pad_y, int pad_x, const float* gat_scale,
                              const float* dir_scale, float* dw, float* work, hipStream_t st);

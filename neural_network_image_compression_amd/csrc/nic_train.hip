@@ -59,6 +59,7 @@ struct GatherArgs {
   const float* sw;     // device scale of the weights or null (already applied in wp)
   float* y;            // [n][oh][ow][cout]
   int n, h, w, cin, oh, ow, cout, kh, kw, stride, pad_y, pad_x, transposed;
+  int act;             // 1: leaky_relu(0.2) of the biased sum (Keras activation=tf.nn.leaky_relu)
   int K;               // kh * kw * cin
   long long M;         // n * oh * ow
   int ph_blk[5];       // phase mode: first block of output phase (py, px) = (p >> 1, p & 1), then the grid
@@ -281,12 +282,105 @@ __global__ __launch_bounds__(256) void conv_gather_kernel(GatherArgs a) {
     f32x4 v;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = (acc[t][r] * isx) * isw + (a.bias && co + r < a.cout ? a.bias[co + r] : 0.f);
+    if (a.act)  // tf.nn.leaky_relu(z, 0.2) = max(0.2 z, z): z for z > 0, else 0.2 z (one rounding)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(__fmul_rn(v[r], 0.2f), v[r]);
     if ((a.cout & 3) == 0 && co + 4 <= a.cout) {
       *(f32x4*)(yp + co) = v;
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (co + r < a.cout) yp[co + r] = v[r];
+    }
+  }
+}
+
+// ---- activation + bias gradient of a layer ------------------------------------------------
+// dz = dy * (act && !(y > 0) ? 0.2 : 1): tf.nn.leaky_relu's gradient (z > 0 ? dy : 0.2 dy),
+// read from the layer's output y (y > 0 iff z > 0); db[c] = sum over rows of dz[row][c]
+// (BiasAddGrad); and the power-of-two operand scale of dz (nic_absmax_scale's, from the same
+// pass).  A block takes kAbgRows rows; thread t owns V consecutive columns (V = 4: 16-B loads
+// when cols % 4 == 0) of row lane t / (cols / V), summed per thread in row order, then over
+// the row lanes in order into part[block][c] (max |dz| into part[nblk * cols + block]);
+// abg_reduce_kernel adds the blocks' partials of a column in a fixed order (deterministic).
+constexpr int kAbgRows = 256;
+template <int V>
+__global__ __launch_bounds__(256) void act_bias_grad_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                                            long long rows, int cols, int act, float* __restrict__ dz,
+                                                            float* __restrict__ part) {
+  typedef float fv __attribute__((ext_vector_type(V)));
+  __shared__ float red[256 * V];
+  __shared__ float wm[4];
+  const int cg = cols / V, nrl = 256 / cg, t = threadIdx.x, c0 = (t % cg) * V, rl = t / cg;
+  const long long r0 = (long long)blockIdx.x * kAbgRows;
+  const long long r1 = r0 + kAbgRows < rows ? r0 + kAbgRows : rows;
+  fv s = {};
+  float m = 0.f;
+  if (rl < nrl) {
+#pragma unroll 4
+    for (long long r = r0 + rl; r < r1; r += nrl) {
+      const long long e = r * cols + c0;
+      fv g = *(const fv*)(dy + e);
+      if (act) {
+        const fv yv = *(const fv*)(y + e);
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (!(yv[k] > 0.f)) g[k] = __fmul_rn(g[k], 0.2f);
+      }
+      if (dz) *(fv*)(dz + e) = g;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        s[k] = __fadd_rn(s[k], g[k]);
+        m = fmaxf(m, fabsf(g[k]));
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) red[t * V + k] = s[k];
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((t & 63) == 0) wm[t >> 6] = m;
+  __syncthreads();
+  if (t < cols) {  // column t: lane group t / V of every row lane, in row-lane order
+    float b = 0.f;
+    for (int k = 0; k < nrl; ++k) b = __fadd_rn(b, red[(k * cg + t / V) * V + t % V]);
+    part[(long long)blockIdx.x * cols + t] = b;
+  }
+  if (t == 0) part[(long long)gridDim.x * cols + blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// Block c < cols: db[c] = sum of the blocks' partials of column c (thread k adds partials k,
+// k + 256, ... in order, then a fixed pairwise tree over the threads); block cols: the scale
+// of the blocks' max |dz| (nic_absmax_scale's formula)
+__global__ __launch_bounds__(256) void abg_reduce_kernel(const float* __restrict__ part, int nblk, int cols,
+                                                         float* __restrict__ db, float* __restrict__ scale) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (c < cols) {
+    if (!db) return;
+    float s = 0.f;
+    for (int k = t; k < nblk; k += 256) s = __fadd_rn(s, part[(long long)k * cols + c]);
+    red[t] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] = __fadd_rn(red[t], red[t + o]);
+      __syncthreads();
+    }
+    if (t == 0) db[c] = red[0];
+  } else {
+    if (!scale) return;
+    float m = 0.f;
+    for (int k = t; k < nblk; k += 256) m = fmaxf(m, part[(long long)nblk * cols + k]);
+    red[t] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] = fmaxf(red[t], red[t + o]);
+      __syncthreads();
+    }
+    if (t == 0) {
+      m = red[0];
+      float sc = 1.0f;
+      if (m > 0.f && isfinite(m)) sc = ldexpf(1.0f, min(max(13 - ilogbf(m), -126), 126));
+      *scale = sc;
     }
   }
 }
@@ -547,10 +641,41 @@ size_t train_gather_work_bytes(int kh, int kw, int cin, int cout) {
   return (size_t)((kh * kw * cin + TK - 1) / TK) * (tile16(cout) / 16) * 2 * 64 * sizeof(f16x8);
 }
 
+size_t train_abg_work_floats(long long rows, int cols) {
+  return (size_t)((rows + kAbgRows - 1) / kAbgRows) * (cols + 1);
+}
+
+hipError_t launch_act_bias_grad(const float* y, const float* dy, long long rows, int cols, int act, float* dz, float* db,
+                                float* dz_scale, float* work, hipStream_t st) {
+  const long long nblk = (rows + kAbgRows - 1) / kAbgRows;
+  if (nblk > INT32_MAX) return hipErrorInvalidValue;
+  if (nblk == 0 && db) {
+    const hipError_t e = hipMemsetAsync(db, 0, (size_t)cols * sizeof(float), st);
+    if (e != hipSuccess) return e;
+  }
+  if (nblk > 0) {
+    const bool vec = cols % 4 == 0 && (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)dz) & 15) == 0;
+    if (vec)
+      hipLaunchKernelGGL(act_bias_grad_kernel<4>, dim3((unsigned)nblk), dim3(256), 0, st, y, dy, rows, cols, act, dz, work);
+    else
+      hipLaunchKernelGGL(act_bias_grad_kernel<1>, dim3((unsigned)nblk), dim3(256), 0, st, y, dy, rows, cols, act, dz, work);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if ((db && nblk > 0) || dz_scale) {  // (an empty tensor's scale: 1)
+    hipLaunchKernelGGL(abg_reduce_kernel, dim3((unsigned)cols + 1), dim3(256), 0, st, work, (int)nblk, cols,
+                       nblk > 0 ? db : nullptr, dz_scale);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, const float* wt, int kh, int kw, int layout,
                               int stride, int pad_y, int pad_x, int transposed, const float* bias, const float* x_scale,
-                              const float* w_scale, float* y, int oh, int ow, int cout, void* work, hipStream_t st) {
+                              const float* w_scale, float* y, int oh, int ow, int cout, int act, void* work,
+                              hipStream_t st) {
   GatherArgs a{};
+  a.act = act;
   a.x = x; a.wp = (const f16x8*)work; a.bias = bias; a.y = y;
   a.sx = x_scale; a.sw = w_scale;
   a.n = n; a.h = h; a.w = w; a.cin = cin; a.oh = oh; a.ow = ow; a.cout = cout; a.kh = kh; a.kw = kw;

@@ -17,9 +17,12 @@ The SSIM loss's separable Gaussian (one-channel VALID correlation) runs on a 1-D
 kernel and its adjoint (``gauss_valid``, ``nic_gauss_1d``).
 
 Each operand gets a power-of-two scale (max |t| * scale in [2^13, 2^14)) computed on the
-device once per tensor (x and the kernel in the forward, dy in the backward), so the f16 hi/lo split keeps tiny gradients exact to ~2^-22.  Bias gradients are
-plain reductions (torch), as are the leaky-ReLU / clip / SSIM elementwise parts.  There is
-no fallback: without the built library these raise.
+device once per tensor (x and the kernel in the forward, dy in the backward), so the f16 hi/lo split keeps tiny gradients exact to ~2^-22.  The layers' leaky-ReLU runs in
+the gather's epilogue (``nic_conv_gather_act``), and its gradient with the bias gradient in
+one deterministic pass (``nic_act_bias_grad``: dz = dy * leaky'(y), db = column sums of dz).
+The clip, residual-add, noise and SSIM elementwise parts and the Entropynet's two dense layers
+(plain library GEMMs) stay on torch.  There is no fallback: without the built library these
+raise.
 """
 from __future__ import annotations
 
@@ -74,9 +77,9 @@ def _check(t, name):
 
 
 def gather(x, wt, layout: int, stride: int, pad: Tuple[int, int], transposed: int, out_hw: Tuple[int, int],
-           cout: int, bias=None, sx=None, sw=None):
-    """nic_conv_gather on NHWC x: returns (n, oh, ow, cout).  sx / sw: operand scales
-    (:func:`scale`), computed here when not given."""
+           cout: int, bias=None, sx=None, sw=None, act: int = 0):
+    """nic_conv_gather_act on NHWC x: returns (n, oh, ow, cout), leaky_relu(0.2)-activated
+    when act.  sx / sw: operand scales (:func:`scale`), computed here when not given."""
     torch = _torch()
     import ctypes
 
@@ -95,10 +98,40 @@ def gather(x, wt, layout: int, stride: int, pad: Tuple[int, int], transposed: in
     bias = _check(bias, "gather bias") if bias is not None else None
     b = bias.data_ptr() if bias is not None else None
     with torch.cuda.device(dev):
-        _lib.check(L.nic_conv_gather(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0], pad[1],
-                                     transposed, b, sx.data_ptr(), sw.data_ptr(), y.data_ptr(), out_hw[0], out_hw[1],
-                                     cout, work.data_ptr(), int(need.value), _stream(dev)), "nic_conv_gather")
+        _lib.check(L.nic_conv_gather_act(x.data_ptr(), n, h, w, cin, wt.data_ptr(), kh, kw, layout, stride, pad[0],
+                                         pad[1], transposed, b, sx.data_ptr(), sw.data_ptr(), y.data_ptr(), out_hw[0],
+                                         out_hw[1], cout, int(act), work.data_ptr(), int(need.value), _stream(dev)),
+                   "nic_conv_gather_act")
     return y
+
+
+ABG_ROWS = 256  # rows per block of nic_act_bias_grad (its work: per block a row of sums and a max)
+
+
+def act_bias_grad(y, dy, act: int, want_dz: bool = True, want_db: bool = True):
+    """nic_act_bias_grad on NHWC tensors: (dz, db, dz_scale) with dz = dy * leaky'(y) (dy itself
+    when not act), db its per-channel sums and dz_scale its operand scale (:func:`scale`), from
+    one pass; dz / db are None when not wanted (dz_scale too, without dz)."""
+    torch = _torch()
+    dy = _check(dy, "act_bias_grad dy")
+    if act:
+        y = _check(y, "act_bias_grad y")
+    dev = _same_device(y if act else None, dy)
+    cols = dy.shape[-1]
+    rows = dy.numel() // cols if cols else 0
+    dz = (torch.empty_like(dy) if act else dy) if want_dz else None
+    if not want_db and not want_dz:
+        return None, None, None
+    db = torch.empty((cols,), dtype=torch.float32, device=dy.device) if want_db else None
+    sdz = torch.empty((1,), dtype=torch.float32, device=dy.device) if want_dz else None
+    need = -(-rows // ABG_ROWS) * (cols + 1)  # nic_act_bias_grad_work (checked by the call)
+    work = torch.empty(max(need, 1), dtype=torch.float32, device=dy.device)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().nic_act_bias_grad(
+            y.data_ptr() if act else None, dy.data_ptr(), rows, cols, int(act),
+            dz.data_ptr() if (dz is not None and act) else None, db.data_ptr() if db is not None else None,
+            sdz.data_ptr() if sdz is not None else None, work.data_ptr(), need, _stream(dev)), "nic_act_bias_grad")
+    return dz, db, sdz
 
 
 def wgrad(gat, dirt, kh: int, kw: int, stride: int, pad: Tuple[int, int], sg=None, sd=None):
@@ -146,60 +179,66 @@ def _conv_fn():
     torch = _torch()
 
     class Conv2DSame(torch.autograd.Function):
-        """Keras Conv2D(padding='SAME') without activation, NHWC; kernel (kh, kw, Cin, Cout)."""
+        """Keras Conv2D(padding='SAME'), leaky_relu(0.2) when act, NHWC; kernel (kh, kw, Cin, Cout)."""
 
         @staticmethod
-        def forward(ctx, x, kernel, bias, stride):
+        def forward(ctx, x, kernel, bias, stride, act):
             x, kernel = _check(x, "Conv2DSame x"), _check(kernel, "Conv2DSame kernel")
             n, h, w, _ = x.shape
             kh, kw, _, cout = kernel.shape
             pt, pl = same_pad(h, kh, stride)[0], same_pad(w, kw, stride)[0]
             oh, ow = -(-h // stride), -(-w // stride)
             sx, sw = scale(x), scale(kernel)
-            ctx.save_for_backward(x, kernel, sx, sw)
-            ctx.geo = (stride, pt, pl)
-            return gather(x, kernel, 0, stride, (pt, pl), 0, (oh, ow), cout, bias, sx, sw)
+            y = gather(x, kernel, 0, stride, (pt, pl), 0, (oh, ow), cout, bias, sx, sw, act=int(act))
+            ctx.save_for_backward(x, kernel, sx, sw, y if act else None)
+            ctx.geo = (stride, pt, pl, bool(act))
+            return y
 
         @staticmethod
         def backward(ctx, dy):
-            x, kernel, sx, sw = ctx.saved_tensors
-            stride, pt, pl = ctx.geo
+            x, kernel, sx, sw, y = ctx.saved_tensors
+            stride, pt, pl, act = ctx.geo
             dy = dy.contiguous()
-            sdy = scale(dy)
+            need_dz = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+            dy, db, sdy = act_bias_grad(y, dy, act, need_dz, ctx.needs_input_grad[2])
+            if not need_dz:
+                return None, None, db, None, None
             kh, kw, cin, _ = kernel.shape
             dx = gather(dy, kernel, 1, stride, (pt, pl), 1, (x.shape[1], x.shape[2]), cin, None, sdy, sw) \
                 if ctx.needs_input_grad[0] else None
             dk = wgrad(x, dy, kh, kw, stride, (pt, pl), sx, sdy) if ctx.needs_input_grad[1] else None
-            db = dy.sum(dim=(0, 1, 2)) if ctx.needs_input_grad[2] else None
-            return dx, dk, db, None
+            return dx, dk, db, None, None
 
     class Conv2DTransposeSame(torch.autograd.Function):
-        """Keras Conv2DTranspose(padding='SAME') without activation, NHWC; kernel (kh, kw, Cout, Cin)."""
+        """Keras Conv2DTranspose(padding='SAME'), leaky_relu(0.2) when act, NHWC; kernel (kh, kw, Cout, Cin)."""
 
         @staticmethod
-        def forward(ctx, x, kernel, bias, stride):
+        def forward(ctx, x, kernel, bias, stride, act):
             x, kernel = _check(x, "Conv2DTransposeSame x"), _check(kernel, "Conv2DTransposeSame kernel")
             n, h, w, _ = x.shape
             kh, kw, cout, _ = kernel.shape
             oh, ow = h * stride, w * stride
             pt, pl = same_pad(oh, kh, stride)[0], same_pad(ow, kw, stride)[0]
             sx, sw = scale(x), scale(kernel)
-            ctx.save_for_backward(x, kernel, sx, sw)
-            ctx.geo = (stride, pt, pl)
-            return gather(x, kernel, 1, stride, (pt, pl), 1, (oh, ow), cout, bias, sx, sw)
+            y = gather(x, kernel, 1, stride, (pt, pl), 1, (oh, ow), cout, bias, sx, sw, act=int(act))
+            ctx.save_for_backward(x, kernel, sx, sw, y if act else None)
+            ctx.geo = (stride, pt, pl, bool(act))
+            return y
 
         @staticmethod
         def backward(ctx, dy):
-            x, kernel, sx, sw = ctx.saved_tensors
-            stride, pt, pl = ctx.geo
+            x, kernel, sx, sw, y = ctx.saved_tensors
+            stride, pt, pl, act = ctx.geo
             dy = dy.contiguous()
-            sdy = scale(dy)
+            need_dz = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+            dy, db, sdy = act_bias_grad(y, dy, act, need_dz, ctx.needs_input_grad[2])
+            if not need_dz:
+                return None, None, db, None, None
             kh, kw, _, cin = kernel.shape
             dx = gather(dy, kernel, 0, stride, (pt, pl), 0, (x.shape[1], x.shape[2]), cin, None, sdy, sw) \
                 if ctx.needs_input_grad[0] else None
             dk = wgrad(dy, x, kh, kw, stride, (pt, pl), sdy, sx) if ctx.needs_input_grad[1] else None
-            db = dy.sum(dim=(0, 1, 2)) if ctx.needs_input_grad[2] else None
-            return dx, dk, db, None
+            return dx, dk, db, None, None
 
     class Gauss1D(torch.autograd.Function):
         """One-channel VALID correlation along x or y with constant taps (nic_gauss_1d), the
@@ -230,18 +269,13 @@ def _fns():
 
 
 def conv_same(x, kernel_hwio, bias, stride: int, act: bool = True):
-    """Keras Conv2D(padding='SAME') + leaky_relu(0.2) on NHWC (HIP)."""
-    import torch.nn.functional as F
-
-    y = _fns()[0].apply(x, kernel_hwio, bias, stride)
-    return F.leaky_relu(y, 0.2) if act else y
+    """Keras Conv2D(padding='SAME') + leaky_relu(0.2) on NHWC (HIP, activation in the epilogue)."""
+    return _fns()[0].apply(x, kernel_hwio, bias, stride, bool(act))
 
 
 def tconv_same(x, kernel_hwoi, bias, stride: int):
-    """Keras Conv2DTranspose(padding='SAME') + leaky_relu(0.2) on NHWC (HIP)."""
-    import torch.nn.functional as F
-
-    return F.leaky_relu(_fns()[1].apply(x, kernel_hwoi, bias, stride), 0.2)
+    """Keras Conv2DTranspose(padding='SAME') + leaky_relu(0.2) on NHWC (HIP, activation in the epilogue)."""
+    return _fns()[1].apply(x, kernel_hwoi, bias, stride, True)
 
 
 def gauss_valid(t, g1d):

@@ -121,3 +121,13 @@ def test_training_entry_points_validate_without_a_gpu():
     assert L.nic_gauss_1d(None, 1, 20, 20, None, 11, 0, 0, None, 20, 9, None) == _lib.NIC_ESHAPE  # 20 - 10 != 9
     assert L.nic_gauss_1d(None, 1, 20, 20, None, 11, 0, 0, None, 20, 10, None) == _lib.NIC_EINVAL
     assert L.nic_absmax_scale(None, -1, None, None, None) == _lib.NIC_ESHAPE
+    # the fused-activation gather and the activation / bias gradient (nic_train.hip)
+    assert L.nic_conv_gather_act(None, 1, 8, 8, 64, None, 3, 3, 0, 1, 1, 1, 0, None, None, None, None, 8, 8, 64, 2,
+                                 None, 0, None) == _lib.NIC_EINVAL  # act not 0 / 1
+    assert L.nic_conv_gather_act(None, 0, 8, 8, 64, None, 3, 3, 0, 1, 1, 1, 0, None, None, None, None, 8, 8, 64, 1,
+                                 None, 0, None) == _lib.NIC_OK
+    assert L.nic_act_bias_grad_work(5000, 64, ctypes.byref(f)) == _lib.NIC_OK and f.value == 20 * 65  # 256-row blocks: 64 sums and a max each
+    assert L.nic_act_bias_grad_work(10, 65, ctypes.byref(f)) == _lib.NIC_ESHAPE
+    assert L.nic_act_bias_grad(None, None, 10, 64, 1, None, None, None, None, 0, None) == _lib.NIC_EINVAL  # no output
+    assert L.nic_act_bias_grad(None, None, 10, 64, 1, None, ctypes.c_void_p(16), None, None, 0, None) == _lib.NIC_EINVAL
+    assert L.nic_act_bias_grad(None, None, -1, 64, 0, None, None, None, None, 0, None) == _lib.NIC_ESHAPE
