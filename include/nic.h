@@ -257,6 +257,12 @@ int nic_unpack_latent(const uint8_t* packed, int n, int h8, int w8, uint8_t* lat
  * nic_gauss_1d: one-channel planes (n,h,w): VALID correlation with ntaps taps along x
  *     (vertical 0) or y, or its adjoint (the input gradient); the SSIM loss's separable
  *     Gaussian (tf.image.ssim, training.py:119-121).
+ * nic_ssim_map: the SSIM loss's map from its Gaussian-filtered terms (tf.image.ssim,
+ *     training.py:119-121): per pixel of n planes of hw pixels, from mx = G*x, my = G*y,
+ *     sxy = G*(x y), sxx = G*(x^2 + y^2): num0 = (mx my) 2, den0 = mx mx + my my,
+ *     lum = (num0 + c1)/(den0 + c1), cs = ((2 sxy - num0) + c2)/((sxx - den0) + c2); ssim_mean[i] =
+ *     mean of lum cs over plane i (deterministic; work >= nic_ssim_map_work() floats).
+ * nic_ssim_map_grad: the gradients of sum_i g[i] ssim_mean[i] with respect to mx, my, sxy, sxx.
  * nic_adam_keras: the step's optimiser update (training.py:147-149, tf.keras Adam = TF's
  *     ResourceApplyAdam) over `count` tensors in one launch; table = device int64 records
  *     {var, m, v, grad, n} (pointers to fp32 device buffers, n elements), max_n their largest n:
@@ -281,6 +287,11 @@ int nic_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, const float*
 int nic_absmax_scale(const float* x, int64_t count, float* scale, float* work, void* stream);
 int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, int ntaps, int vertical, int adjoint,
                  float* out, int h_out, int w_out, void* stream);
+int nic_ssim_map_work(int n, int64_t hw, int64_t* floats);
+int nic_ssim_map(const float* mx, const float* my, const float* sxy, const float* sxx, int n, int64_t hw, float c1,
+                 float c2, float* ssim_mean, float* work, int64_t work_floats, void* stream);
+int nic_ssim_map_grad(const float* mx, const float* my, const float* sxy, const float* sxx, const float* g, int n,
+                      int64_t hw, float c1, float c2, float* gmx, float* gmy, float* gsxy, float* gsxx, void* stream);
 int nic_adam_keras(const int64_t* table, int count, int64_t max_n, float alpha, float beta1, float beta2,
                    float epsilon, void* stream);
 

@@ -93,6 +93,11 @@ _SIGNATURES = {
     "nic_absmax_scale": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp, c_vp]),
     "nic_gauss_1d": (ctypes.c_int, [c_vp] + [ctypes.c_int] * 3 + [c_vp] + [ctypes.c_int] * 3 + [c_vp]
                      + [ctypes.c_int] * 2 + [c_vp]),
+    "nic_ssim_map_work": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "nic_ssim_map": (ctypes.c_int, [c_vp] * 4 + [ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_float]
+                     + [c_vp, c_vp, ctypes.c_int64, c_vp]),
+    "nic_ssim_map_grad": (ctypes.c_int, [c_vp] * 5 + [ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_float]
+                          + [c_vp] * 5),
     "nic_adam_keras": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int64] + [ctypes.c_float] * 4 + [c_vp]),
 }
 

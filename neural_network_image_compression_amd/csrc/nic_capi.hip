@@ -1480,6 +1480,35 @@ int nic_gauss_1d(const float* in, int n, int h_in, int w_in, const float* taps, 
   return NIC_OK;
 }
 
+int nic_ssim_map_work(int n, int64_t hw, int64_t* floats) {
+  if (!floats) return fail(NIC_EINVAL, "nic_ssim_map_work: NULL argument");
+  if (n < 0 || hw <= 0) return fail(NIC_ESHAPE, "nic_ssim_map_work: bad shape");
+  *floats = (int64_t)train_ssim_work_floats(n, hw);
+  return NIC_OK;
+}
+
+int nic_ssim_map(const float* mx, const float* my, const float* sxy, const float* sxx, int n, int64_t hw, float c1,
+                 float c2, float* ssim_mean, float* work, int64_t work_floats, void* stream) {
+  if (n < 0 || hw <= 0 || (int64_t)n * hw > ((int64_t)1 << 40)) return fail(NIC_ESHAPE, "nic_ssim_map: bad shape");
+  if (n == 0) return NIC_OK;
+  if (!mx || !my || !sxy || !sxx || !ssim_mean || !work) return fail(NIC_EINVAL, "nic_ssim_map: NULL argument");
+  if (work_floats < (int64_t)train_ssim_work_floats(n, hw))
+    return fail(NIC_EINVAL, "nic_ssim_map: work holds %lld floats, needs %lld", (long long)work_floats,
+                (long long)train_ssim_work_floats(n, hw));
+  HIP_TRY(launch_ssim_map(mx, my, sxy, sxx, n, hw, c1, c2, ssim_mean, work, (hipStream_t)stream));
+  return NIC_OK;
+}
+
+int nic_ssim_map_grad(const float* mx, const float* my, const float* sxy, const float* sxx, const float* g, int n,
+                      int64_t hw, float c1, float c2, float* gmx, float* gmy, float* gsxy, float* gsxx, void* stream) {
+  if (n < 0 || hw <= 0 || (int64_t)n * hw > ((int64_t)1 << 40)) return fail(NIC_ESHAPE, "nic_ssim_map_grad: bad shape");
+  if (n == 0) return NIC_OK;
+  if (!mx || !my || !sxy || !sxx || !g || !gmx || !gmy || !gsxy || !gsxx)
+    return fail(NIC_EINVAL, "nic_ssim_map_grad: NULL argument");
+  HIP_TRY(launch_ssim_map_grad(mx, my, sxy, sxx, g, n, hw, c1, c2, gmx, gmy, gsxy, gsxx, (hipStream_t)stream));
+  return NIC_OK;
+}
+
 int nic_adam_keras(const int64_t* table, int count, int64_t max_n, float alpha, float beta1, float beta2,
                    float epsilon, void* stream) {
   if (count < 0 || count > 65535 || max_n < 0) return fail(NIC_ESHAPE, "nic_adam_keras: bad count %d / max_n %lld", count, (long long)max_n);

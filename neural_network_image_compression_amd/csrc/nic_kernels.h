@@ -218,6 +218,12 @@ hipError_t launch_conv_wgrad(const float* gat, int n, int gh, int gw, int ca, co
 // tf.keras Adam over `count` tensors (table: {var, m, v, grad, n} int64 records on the device)
 hipError_t launch_adam_keras(const long long* table, int count, long long max_n, float alpha, float beta1,
                              float beta2, float eps, hipStream_t st);
+size_t train_ssim_work_floats(int n, long long hw);
+hipError_t launch_ssim_map(const float* mx, const float* my, const float* sxy, const float* sxx, int n, long long hw,
+                           float c1, float c2, float* out, float* work, hipStream_t st);
+hipError_t launch_ssim_map_grad(const float* mx, const float* my, const float* sxy, const float* sxx, const float* g,
+                                int n, long long hw, float c1, float c2, float* gmx, float* gmy, float* gsxy,
+                                float* gsxx, hipStream_t st);
 hipError_t launch_gauss1d(const float* in, int n, int hi, int wi, const float* taps, int nt, int vertical, int adjoint,
                           float* out, int ho, int wo, hipStream_t st);
 

@@ -385,6 +385,80 @@ __global__ __launch_bounds__(256) void abg_reduce_kernel(const float* __restrict
   }
 }
 
+// ---- SSIM map of the loss from its filtered terms (tf.image.ssim, training.py:119-121) ------
+// Per pixel of the VALID map, from mx = G*x, my = G*y, sxy = G*(x y), sxx = G*(x^2 + y^2):
+//   num0 = (mx my) 2, den0 = mx mx + my my, lum = (num0 + c1) / (den0 + c1),
+//   cs = ((2 sxy - num0) + c2) / ((sxx - den0) + c2), v = lum cs
+// in tf.image.ssim's op order, every op rounded; forward: the per-image mean of v (per-block
+// partial sums in pixel order, then added in block order: deterministic); backward: the four
+// terms' gradients of g[n] * mean.
+constexpr int kSsimPix = 1024;  // map pixels per block
+struct SsimTerms {
+  float num0, den0, lum, cs, a, b, c, d;
+};
+__device__ __forceinline__ SsimTerms ssim_terms(float mx, float my, float sxy, float sxx, float c1, float c2) {
+  SsimTerms t;
+  t.num0 = __fmul_rn(__fmul_rn(mx, my), 2.0f);
+  t.den0 = __fadd_rn(__fmul_rn(mx, mx), __fmul_rn(my, my));
+  t.a = __fadd_rn(t.num0, c1);
+  t.b = __fadd_rn(t.den0, c1);
+  t.lum = __fdiv_rn(t.a, t.b);
+  t.c = __fadd_rn(__fsub_rn(__fmul_rn(sxy, 2.0f), t.num0), c2);
+  t.d = __fadd_rn(__fsub_rn(sxx, t.den0), c2);
+  t.cs = __fdiv_rn(t.c, t.d);
+  return t;
+}
+__global__ __launch_bounds__(256) void ssim_map_kernel(const float* __restrict__ mx, const float* __restrict__ my,
+                                                       const float* __restrict__ sxy, const float* __restrict__ sxx,
+                                                       long long hw, int bpi, float c1, float c2,
+                                                       float* __restrict__ part) {
+  __shared__ float red[256];
+  const int n = blockIdx.x / bpi, bk = blockIdx.x - n * bpi, t = threadIdx.x;
+  const long long base = (long long)n * hw, p0 = (long long)bk * kSsimPix;
+  float s = 0.f;
+  for (long long p = p0 + t; p < p0 + kSsimPix && p < hw; p += 256) {
+    const long long e = base + p;
+    const SsimTerms q = ssim_terms(mx[e], my[e], sxy[e], sxx[e], c1, c2);
+    s = __fadd_rn(s, __fmul_rn(q.lum, q.cs));
+  }
+  red[t] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] = __fadd_rn(red[t], red[t + o]);
+    __syncthreads();
+  }
+  if (t == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(64) void ssim_mean_kernel(const float* __restrict__ part, int n, int bpi, long long hw,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < bpi; ++k) s = __fadd_rn(s, part[(long long)i * bpi + k]);
+  out[i] = __fdiv_rn(s, (float)hw);
+}
+__global__ __launch_bounds__(256) void ssim_map_grad_kernel(const float* __restrict__ mx, const float* __restrict__ my,
+                                                            const float* __restrict__ sxy, const float* __restrict__ sxx,
+                                                            const float* __restrict__ g, int n, long long hw, float c1,
+                                                            float c2, float* __restrict__ gmx, float* __restrict__ gmy,
+                                                            float* __restrict__ gsxy, float* __restrict__ gsxx) {
+  const long long total = (long long)n * hw;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const float x = mx[e], y = my[e];
+    const SsimTerms q = ssim_terms(x, y, sxy[e], sxx[e], c1, c2);
+    const float G = __fdiv_rn(g[e / hw], (float)hw);  // d mean / d v
+    // v = (a / b) (c / d): dv/dnum0 = cs / b - lum / d, dv/dden0 = lum cs / d - lum cs / b,
+    // dv/d(2 sxy) = lum / d, dv/dsxx = -lum cs / d
+    const float ib = __frcp_rn(q.b), id = __frcp_rn(q.d), v = __fmul_rn(q.lum, q.cs);
+    const float dnum0 = __fmul_rn(G, __fsub_rn(__fmul_rn(q.cs, ib), __fmul_rn(q.lum, id)));
+    const float dden0 = __fmul_rn(G, __fsub_rn(__fmul_rn(v, id), __fmul_rn(v, ib)));
+    gmx[e] = __fmul_rn(2.0f, __fadd_rn(__fmul_rn(dnum0, y), __fmul_rn(dden0, x)));
+    gmy[e] = __fmul_rn(2.0f, __fadd_rn(__fmul_rn(dnum0, x), __fmul_rn(dden0, y)));
+    gsxy[e] = __fmul_rn(2.0f, __fmul_rn(G, __fmul_rn(q.lum, id)));
+    gsxx[e] = -__fmul_rn(G, __fmul_rn(v, id));
+  }
+}
+
 // ---- separable Gaussian of the SSIM loss (tf.image.ssim's 11-tap window) --------------------
 // One-channel planes (n, h, w): VALID correlation along x (vertical = 0) or y, or its adjoint
 // (the input gradient: a full convolution with the same taps).
@@ -712,6 +786,32 @@ hipError_t launch_conv_gather(const float* x, int n, int h, int w, int cin, cons
     case 65: return launch_gather_t<64, true, false>(a, st);
     default: return launch_gather_t<64, true, true>(a, st);
   }
+}
+
+size_t train_ssim_work_floats(int n, long long hw) { return (size_t)n * ((hw + kSsimPix - 1) / kSsimPix); }
+
+hipError_t launch_ssim_map(const float* mx, const float* my, const float* sxy, const float* sxx, int n, long long hw,
+                           float c1, float c2, float* out, float* work, hipStream_t st) {
+  const long long bpi = (hw + kSsimPix - 1) / kSsimPix;
+  if (n == 0) return hipSuccess;
+  if (bpi * n > INT32_MAX || bpi > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ssim_map_kernel, dim3((unsigned)(bpi * n)), dim3(256), 0, st, mx, my, sxy, sxx, hw, (int)bpi, c1,
+                     c2, work);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ssim_mean_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, work, n, (int)bpi, hw, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ssim_map_grad(const float* mx, const float* my, const float* sxy, const float* sxx, const float* g,
+                                int n, long long hw, float c1, float c2, float* gmx, float* gmy, float* gsxy,
+                                float* gsxx, hipStream_t st) {
+  const long long total = (long long)n * hw;
+  if (total == 0) return hipSuccess;
+  const long long blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(ssim_map_grad_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, st, mx, my,
+                     sxy, sxx, g, n, hw, c1, c2, gmx, gmy, gsxy, gsxx);
+  return hipGetLastError();
 }
 
 hipError_t launch_gauss1d(const float* in, int n, int hi, int wi, const float* taps, int nt, int vertical, int adjoint,

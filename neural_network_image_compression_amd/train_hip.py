@@ -255,7 +255,40 @@ def _conv_fn():
             (taps,) = ctx.saved_tensors
             return gauss_1d(dy.contiguous(), taps, ctx.vertical, 1), None, None
 
-    return Conv2DSame, Conv2DTransposeSame, Gauss1D
+    class SsimMap(torch.autograd.Function):
+        """Per-plane mean of tf.image.ssim's map from its filtered terms (nic_ssim_map /
+        nic_ssim_map_grad): mx, my, sxy = G*(x y), sxx = G*(x^2 + y^2), each (N, ...) planes."""
+
+        @staticmethod
+        def forward(ctx, mx, my, sxy, sxx, c1, c2):
+            ts = [_check(t, "SsimMap term") for t in (mx, my, sxy, sxx)]
+            dev = _same_device(*ts)
+            n = ts[0].shape[0]
+            hw = ts[0].numel() // max(n, 1)
+            out = torch.empty((n,), dtype=torch.float32, device=ts[0].device)
+            need = n * (-(-hw // SSIM_PIX))  # nic_ssim_map_work (checked by the call)
+            work = torch.empty(max(need, 1), dtype=torch.float32, device=ts[0].device)
+            with torch.cuda.device(dev):
+                _lib.check(_lib.lib().nic_ssim_map(*(t.data_ptr() for t in ts), n, hw, c1, c2, out.data_ptr(),
+                                                   work.data_ptr(), need, _stream(dev)), "nic_ssim_map")
+            ctx.save_for_backward(*ts)
+            ctx.consts = (c1, c2, n, hw)
+            return out
+
+        @staticmethod
+        def backward(ctx, g):
+            ts = ctx.saved_tensors
+            c1, c2, n, hw = ctx.consts
+            g = g.contiguous()
+            grads = [torch.empty_like(t) for t in ts]
+            dev = ts[0].device
+            with torch.cuda.device(dev):
+                _lib.check(_lib.lib().nic_ssim_map_grad(*(t.data_ptr() for t in ts), g.data_ptr(), n, hw, c1, c2,
+                                                        *(t.data_ptr() for t in grads), _stream(dev)),
+                           "nic_ssim_map_grad")
+            return (*grads, None, None)
+
+    return Conv2DSame, Conv2DTransposeSame, Gauss1D, SsimMap
 
 
 _FNS = None
@@ -276,6 +309,14 @@ def conv_same(x, kernel_hwio, bias, stride: int, act: bool = True):
 def tconv_same(x, kernel_hwoi, bias, stride: int):
     """Keras Conv2DTranspose(padding='SAME') + leaky_relu(0.2) on NHWC (HIP, activation in the epilogue)."""
     return _fns()[1].apply(x, kernel_hwoi, bias, stride, True)
+
+
+SSIM_PIX = 1024  # map pixels per block of nic_ssim_map (its work: one partial sum per block)
+
+
+def ssim_map_mean(mx, my, sxy, sxx, c1: float, c2: float):
+    """(N,) per-plane mean of tf.image.ssim's map from its filtered terms (HIP, differentiable)."""
+    return _fns()[3].apply(mx, my, sxy, sxx, float(c1), float(c2))
 
 
 def gauss_valid(t, g1d):

@@ -124,7 +124,7 @@ def _gauss_window(torch, device, dtype, size: int = 11, sigma: float = 1.5):
 def ssim(x, y, max_val: float = 1.0, hip: bool = False):
     """tf.image.ssim (11x11 Gaussian sigma 1.5, k1 0.01, k2 0.03, VALID) of NCHW planes ->
     (N,) mean over the valid map and channels; differentiable.  ``hip``: the Gaussian runs on
-    the HIP gather GEMM (one-channel planes)."""
+    the HIP 1-D kernel and the map's arithmetic with its mean on nic_ssim_map (one-channel planes)."""
     torch = _torch()
     import torch.nn.functional as F
 
@@ -141,6 +141,10 @@ def ssim(x, y, max_val: float = 1.0, hip: bool = False):
 
     c1, c2 = (0.01 * max_val) ** 2, (0.03 * max_val) ** 2
     mx, my = filt(x), filt(y)
+    if hip and c == 1:  # the map and its mean (and their gradients) in one HIP pass each
+        from . import train_hip
+
+        return train_hip.ssim_map_mean(mx, my, filt(x * y), filt(x * x + y * y), c1, c2)
     num0 = mx * my * 2.0
     den0 = mx * mx + my * my
     lum = (num0 + c1) / (den0 + c1)

@@ -131,3 +131,8 @@ def test_training_entry_points_validate_without_a_gpu():
     assert L.nic_act_bias_grad(None, None, 10, 64, 1, None, None, None, None, 0, None) == _lib.NIC_EINVAL  # no output
     assert L.nic_act_bias_grad(None, None, 10, 64, 1, None, ctypes.c_void_p(16), None, None, 0, None) == _lib.NIC_EINVAL
     assert L.nic_act_bias_grad(None, None, -1, 64, 0, None, None, None, None, 0, None) == _lib.NIC_ESHAPE
+    assert L.nic_ssim_map_work(3, 5000, ctypes.byref(f)) == _lib.NIC_OK and f.value == 3 * 5  # 1,024-pixel blocks
+    assert L.nic_ssim_map(None, None, None, None, 3, 0, 1e-4, 9e-4, None, None, 0, None) == _lib.NIC_ESHAPE
+    assert L.nic_ssim_map(None, None, None, None, 3, 100, 1e-4, 9e-4, None, None, 0, None) == _lib.NIC_EINVAL
+    assert L.nic_ssim_map_grad(None, None, None, None, None, 0, 100, 1e-4, 9e-4, None, None, None, None,
+                               None) == _lib.NIC_OK  # no planes

@@ -193,6 +193,27 @@ def test_ssim_gaussian_on_hip_matches_float64():
     assert _rel_err(xd.grad, xr.grad) <= 1e-4
 
 
+def test_ssim_map_fused_matches_float64_both_inputs():
+    # the map's arithmetic and per-plane mean in one HIP pass (nic_ssim_map) and its backward
+    # (nic_ssim_map_grad), weighted per plane, gradients to both images, a training-size plane
+    g = torch.Generator().manual_seed(12)
+    x = torch.rand((4, 1, 128, 128), generator=g)
+    y = (x + 0.1 * torch.randn(x.shape, generator=g)).clamp(0, 1)
+    wts = torch.tensor([1.0, -0.5, 2.0, 0.25])
+    xd, yd = x.cuda().requires_grad_(), y.cuda().requires_grad_()
+    s_hip = T.ssim(xd, yd, hip=True)
+    (s_hip * wts.cuda()).sum().backward()
+    xr, yr = x.double().requires_grad_(), y.double().requires_grad_()
+    s_ref = T.ssim(xr, yr)
+    (s_ref * wts.double()).sum().backward()
+    assert _rel_err(s_hip, s_ref) <= TOL
+    assert _rel_err(xd.grad, xr.grad) <= 1e-4 and _rel_err(yd.grad, yr.grad) <= 1e-4
+    # deterministic
+    xd2 = x.cuda().requires_grad_()
+    s2 = T.ssim(xd2, yd.detach(), hip=True)
+    assert torch.equal(s2, s_hip.detach())
+
+
 def test_strided_operands_and_scale():
     """A strided view (not contiguous) gives the same scale and the same convolution as its
     contiguous copy: the C-ABI reads data_ptr() / numel() of a contiguous tensor only."""
