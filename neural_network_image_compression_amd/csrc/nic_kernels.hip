@@ -1623,8 +1623,9 @@ __global__ __launch_bounds__(256) void colour_split_kernel(const uint8_t* __rest
     }
     const size_t o = ((size_t)k * N + n) * plane + (size_t)yp * wp + 4 * q4;  // 8-B aligned
     typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-    *(u32x2v*)(cp + o) = (u32x2v){hw[0], hw[1]};
-    *(u32x2v*)(cp + P * plane + o) = (u32x2v){lw[0], lw[1]};
+    // nontemporal: 20.4 vs 21.6 us per launch, conv12 unchanged (profiles/r6_ab_logs.txt r6cs)
+    __builtin_nontemporal_store((u32x2v){hw[0], hw[1]}, (u32x2v*)(cp + o));
+    __builtin_nontemporal_store((u32x2v){lw[0], lw[1]}, (u32x2v*)(cp + P * plane + o));
   }
 }
 
