@@ -123,6 +123,32 @@ def test_fused_activation_is_torch_leaky_bit_for_bit():
     assert torch.equal(bd.grad, db1)
 
 
+def test_act_bias_grad_edges():
+    # nic_act_bias_grad: the vector (16-B) and scalar paths (a buffer offset by one float takes
+    # the scalar one) give the same dz and scale bit for bit and the same bias sums (in another
+    # order); one column; an empty tensor (db = 0, scale = 1)
+    from neural_network_image_compression_amd import train_hip
+
+    g = torch.Generator().manual_seed(13)
+    for cols in (64, 32, 1):
+        y = torch.randn((3, 17, 9, cols), generator=g).cuda()
+        dy = torch.randn((3, 17, 9, cols), generator=g).cuda()
+        dz, db, sdz = train_hip.act_bias_grad(y, dy, 1)
+        ref = dy * torch.where(y > 0, torch.ones_like(y), torch.full_like(y, 0.2))
+        assert torch.equal(dz, ref)
+        assert torch.allclose(db, ref.sum(dim=(0, 1, 2)), rtol=1e-5, atol=1e-5)
+        assert torch.equal(sdz, train_hip.scale(ref))
+        by, bdy = torch.empty(y.numel() + 1, device="cuda"), torch.empty(dy.numel() + 1, device="cuda")
+        by[1:].copy_(y.flatten())
+        bdy[1:].copy_(dy.flatten())
+        dz2, db2, sdz2 = train_hip.act_bias_grad(by[1:].view(y.shape), bdy[1:].view(dy.shape), 1)
+        assert torch.equal(dz2, dz) and torch.equal(sdz2, sdz)
+        assert torch.allclose(db2, db, rtol=1e-5, atol=1e-5)
+    e = torch.empty((0, 4, 4, 64), device="cuda")
+    dz, db, sdz = train_hip.act_bias_grad(e, e, 1)
+    assert dz.numel() == 0 and torch.equal(db, torch.zeros(64, device="cuda")) and float(sdz) == 1.0
+
+
 @pytest.mark.parametrize("gscale", [1e-9, 1e6])
 def test_operand_scales_keep_tiny_and_large_gradients(gscale):
     # power-of-two operand scales: a 1e-9 gradient (below f16's smallest subnormal) and a
